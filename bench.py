@@ -1,0 +1,188 @@
+"""Benchmark: Fetch FK + 6x8 geometric Jacobian evaluations per second (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): 2^20 Fetch arm configurations
+per GPU, fp32, world pose of gripper_link (3x4) + 6x8 geometric Jacobian
+(with_rot=true, rpy_jac=false, no base).  One step = one launch of the engine
+over the whole batch; inputs are resident in HBM before timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 1048576]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Multi-GPU: configurations are independent, each rank evaluates its own 2^20
+slice of one global counter-hashed dataset (weak scaling, no collective in the
+timed region besides the bracketing barriers).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
+
+import kinhip  # noqa: E402
+
+ARM = kinhip.FETCH_ARM_JOINTS
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+EXAMPLE_LINKS = ["l_gripper_finger_link", "r_gripper_finger_link", "wrist_flex_link", "wrist_roll_link",
+                 "shoulder_lift_link", "upperarm_roll_link"]
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, ws, local
+    torch.cuda.set_device(local)
+    return None, rank, ws, local
+
+
+def _time_plan(plan, Q, poses, jac, steps, warmup, dist, stream):
+    """K back-to-back launches bracketed by barrier + synchronize; HIP events on the launch stream."""
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            plan.run(Q, poses, jac, stream=stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        plan.run(Q, poses, jac, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_s = e0.elapsed_time(e1) / 1e3
+    t = torch.tensor([wall, dev_s], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]), float(t[1])
+
+
+def _cpu_baseline(m, N_budget_s=12.0):
+    """Reference-faithful C restatement (oracle/kin_oracle.c) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    tree = O.parse_urdf_tree(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+    om = O.OracleMech(tree)
+    ids = [tree.joint_id(n) for n in ARM]
+    gl = tree.link_id("gripper_link")
+    threads = int(os.environ.get("KIN_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    arm = [m.find_joint(n) for n in ARM]
+    chunk = 1 << 16
+    q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], chunk,
+                               dtype=torch.float64).numpy()
+    om.fk_jac_batch(q[:, :1024], ids, gl, ids, True, False, n_threads=threads)  # warm
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < N_budget_s:
+        om.fk_jac_batch(q, ids, gl, ids, True, False, n_threads=threads)
+        done += chunk
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} Fetch configs (chunks of {chunk}) through or_fk_jac_batch: per-config "
+                      f"Mechanism state, cache invalidate, quaternion joint transforms, dense 4x4 fp64 "
+                      f"(src/algorithm.jl restated), {threads} OpenMP threads, {dt:.1f} s"}
+
+
+def _pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_fk_jac_f32.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--n", type=int, default=1 << 20, help="configurations per GPU")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--extras", type=int, default=1, help="also time fp64 FK+J and config-2 FK")
+    args = ap.parse_args()
+
+    dist, rank, ws, local = _dist()
+    dev = torch.device("cuda", local)
+    m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+    arm = [m.find_joint(n) for n in ARM]
+    gl = m.find_link("gripper_link")
+    N = args.n
+    lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
+    stream = torch.cuda.Stream(dev)
+
+    def leg(dtype, jac, links):
+        plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
+                      with_rot=True, dtype=dtype)
+        Q = kinhip.uniform_configs(lo, hi, N, start=rank * N, dtype=dtype, device=dev)
+        poses = torch.empty((len(links), 12, N), dtype=dtype, device=dev)
+        J = torch.empty((8, 6, N), dtype=dtype, device=dev) if jac else None
+        return plan, Q, poses, J
+
+    # ---- headline: FK + J, fp32 -------------------------------------------------
+    plan, Q, poses, J = leg(torch.float32, True, [gl])
+    wall, dev_s = _time_plan(plan, Q, poses, J, args.steps, args.warmup, dist, stream)
+    evals = N * ws * args.steps
+    value = evals / wall
+    bytes_per_eval = (8 + 12 + 48) * 4  # q in + pose + J out (algorithmic)
+    t_launch = dev_s / args.steps
+    achieved = bytes_per_eval * N / t_launch / 1e9
+    traffic = _pmc_traffic()
+    out = {
+        "metric": "FK+Jacobian evals/sec, Fetch URDF, batch=1M, at 1/2/4/8 MI355X",
+        "value": value, "unit": "evals/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (counter-hashed uniform joint angles within "
+                                                       "fetch.urdf limits, seed 20261015)",
+        "config": {"workload": "fetch_fk_jac_gripper_link (BASELINE configs[2])", "urdf": "fetch",
+                   "batch_per_gpu": N, "global_batch": N * ws, "q_joints": 8, "jacobian": "6x8 geometric",
+                   "parallelism": f"dp{ws} (independent shards)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_fk<float,8>", "algorithmic_bytes_per_eval": bytes_per_eval,
+                     "avg_launch_us": t_launch * 1e6},
+    }
+    if args.extras:
+        # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
+        p64, Q64, P64, J64 = leg(torch.float64, True, [gl])
+        w64, d64 = _time_plan(p64, Q64, P64, J64, max(5, args.steps // 2), 3, dist, stream)
+        out["fp64_fk_jac"] = {"value": N * ws * max(5, args.steps // 2) / w64, "unit": "evals/s",
+                              "avg_launch_us": d64 / max(5, args.steps // 2) * 1e6,
+                              "achieved_GBs": 544 * N / (d64 / max(5, args.steps // 2)) / 1e9}
+        del p64, Q64, P64, J64
+        links = [m.find_link(n) for n in EXAMPLE_LINKS]
+        p2, Q2, P2, _ = leg(torch.float64, False, links)
+        w2, d2 = _time_plan(p2, Q2, P2, None, max(5, args.steps // 2), 3, dist, stream)
+        k2 = max(5, args.steps // 2)
+        out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
+                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9}
+        del p2, Q2, P2
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = _cpu_baseline(m)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

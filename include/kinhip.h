@@ -1,0 +1,214 @@
+/*
+ * kinhip.h -- C-ABI of the MI355X batched kinematics engine (libkinhip.so).
+ *
+ * Drop-in boundary for Kinematics.jl's hot path.  The reference has no FFI
+ * layer (it is pure Julia); these entry points are what a Julia `ccall` shim
+ * (kinematics.jl_amd/julia/KinematicsHIP.jl) binds in place of
+ * the Julia methods cited on each declaration.  Plain C types only: device
+ * pointers and sizes in, status codes out, never an exception.
+ *
+ * Conventions
+ *  - Link / joint ids are 1-based, exactly `link.id` / `joint.id` of the
+ *    reference (ids follow URDF document order, src/load_urdf.jl:22-32).
+ *  - Transforms crossing the boundary on the host are 4x4 column-major
+ *    (`Transform.mat`, src/transform.jl:3-5).
+ *  - Batched device arrays are structure-of-arrays with the configuration
+ *    index fastest = Julia column-major `Matrix{T}(N, k)` / `Array{T,3}(N, r, c)`,
+ *    so `pointer(A)` passes zero-copy:
+ *      q      : column c at q[c*ldq + i]; columns = the plan's q joints in order,
+ *               then (x, y, theta) if the model was created with_base.
+ *      poses  : [n_out][12][ldp]; the 12 values are the 3x4 column-major top of
+ *               the 4x4 (R11 R21 R31 R12 R22 R32 R13 R23 R33 tx ty tz).
+ *      jac    : [n_cols][rows][ldj]; rows = 6 (with_rot) or 3; n_cols = n_jac
+ *               (+3 base columns if with_base) -- get_jacobian!'s mat_out.
+ *  - dtype selects float (KIN_F32) or double (KIN_F64) for every batched array
+ *    of one call.  Host-side tree data is always double.
+ *  - Every batched call is asynchronous on the given hipStream_t (passed as
+ *    void*; NULL = the null stream) and capture-safe (no allocation, copy or
+ *    synchronisation inside).
+ *  - Errors: a negative kin_status; kin_last_error() returns a thread-local
+ *    message.  Reference exceptions map to: KeyError -> KIN_E_KEY,
+ *    MethodError (Jacobian column of a fixed joint) -> KIN_E_METHOD,
+ *    throw(Exception) on an unknown URDF joint type -> KIN_E_PARSE.
+ *  - Thread safety: models/plans are immutable after creation except through
+ *    kin_model_set_angles / kin_model_add_link (not concurrent with use).
+ *    Distinct streams may run plans concurrently from different host threads.
+ */
+#ifndef KINHIP_H
+#define KINHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KINHIP_API __attribute__((visibility("default")))
+#define KINHIP_ABI_VERSION 1
+
+typedef enum {
+    KIN_OK = 0,
+    KIN_E_INVALID = -1,     /* bad argument / malformed tree */
+    KIN_E_KEY = -2,         /* unknown link / joint id or name (Julia KeyError) */
+    KIN_E_METHOD = -3,      /* no method (Jacobian column of a relevant fixed joint) */
+    KIN_E_DEVICE = -4,      /* HIP runtime error */
+    KIN_E_UNSUPPORTED = -5, /* outside the engine's limits (see kin_limits) */
+    KIN_E_NOMEM = -6,
+    KIN_E_PARSE = -7,       /* URDF parse error / unsupported joint type */
+    KIN_E_IO = -8
+} kin_status;
+
+typedef enum { KIN_F32 = 0, KIN_F64 = 1 } kin_dtype;
+
+enum { KIN_JOINT_FIXED = 0, KIN_JOINT_REVOLUTE = 1, KIN_JOINT_PRISMATIC = 2 };
+
+/* get_jacobian! keyword/positional flags (src/algorithm.jl:83-88) */
+enum {
+    KIN_WITH_ROT = 1u,  /* rows 4:6 present (with_rot) */
+    KIN_RPY_JAC = 2u,   /* rows 4:6 are d(rpy)/dt (rpy_jac=true) */
+    KIN_ZERO_FILL = 4u  /* get_jacobian (zeros) instead of get_jacobian! (untouched) */
+};
+
+/* ------------------------------------------------------------------------- */
+/* Library                                                                    */
+/* ------------------------------------------------------------------------- */
+KINHIP_API int kin_abi_version(void);
+KINHIP_API const char* kin_last_error(void);
+/* Engine limits: max phase-A chain steps, max Jacobian columns, max outputs. */
+KINHIP_API int kin_limits(int32_t* max_chain, int32_t* max_jac_cols, int32_t* max_slots);
+
+/* ------------------------------------------------------------------------- */
+/* Model = the kinematic tree of a Mechanism (src/mechanism.jl:147-181)       */
+/* ------------------------------------------------------------------------- */
+typedef struct kin_tree_desc {
+    int32_t n_links;
+    int32_t n_joints;
+    const int32_t* joint_type;  /* [n_joints] KIN_JOINT_* (continuous = revolute) */
+    const int32_t* joint_plink; /* [n_joints] 1-based parent link id */
+    const int32_t* joint_clink; /* [n_joints] 1-based child link id */
+    const double* joint_pose;   /* [n_joints][16] 4x4 column-major (Joint.pose) */
+    const double* joint_axis;   /* [n_joints][3]  (Revolute/Prismatic .axis) */
+    const double* joint_lower;  /* [n_joints] or NULL (= -Inf) */
+    const double* joint_upper;  /* [n_joints] or NULL (= +Inf) */
+    int32_t with_base;          /* Mechanism.with_base: planar base (x, y, theta) */
+} kin_tree_desc;
+
+typedef struct kin_model kin_model;
+
+/* Mechanism(...) constructor + create_rptable: src/mechanism.jl:117-139, 166-181.
+ * Stages nothing on the device yet (plans do). */
+KINHIP_API int kin_model_create(const kin_tree_desc* desc, kin_model** out);
+KINHIP_API int kin_model_destroy(kin_model* m);
+KINHIP_API int kin_model_num_links(const kin_model* m, int32_t* out);
+KINHIP_API int kin_model_num_joints(const kin_model* m, int32_t* out);
+/* m.angles for joints NOT driven by a batch column (set_joint_angle(s),
+ * src/mechanism.jl:199-231).  angles: [n_joints] or NULL (zeros). Plans created
+ * afterwards bake these values in; existing plans keep theirs. */
+KINHIP_API int kin_model_set_angles(kin_model* m, const double* angles);
+/* is_relevant(m, joint, link): src/mechanism.jl:277 */
+KINHIP_API int kin_model_is_relevant(const kin_model* m, int32_t joint_id, int32_t link_id, int32_t* out);
+/* add_new_link(m, new_link, parent, pose): src/mechanism.jl:238-267.
+ * Appends a link and a fixed joint named after it; returns the new link id. */
+KINHIP_API int kin_model_add_link(kin_model* m, int32_t parent_link_id, const double* pose16,
+                                  int32_t* new_link_id);
+
+/* ------------------------------------------------------------------------- */
+/* URDF (host; replaces parse_urdf's skrobot call, src/load_urdf.jl:20-80)     */
+/* ------------------------------------------------------------------------- */
+typedef struct kin_urdf kin_urdf;
+KINHIP_API int kin_urdf_parse_file(const char* path, kin_urdf** out);
+KINHIP_API int kin_urdf_parse_string(const char* xml, size_t len, kin_urdf** out);
+KINHIP_API int kin_urdf_destroy(kin_urdf* u);
+/* Tree of the parsed URDF; the pointers stay valid for the lifetime of u.
+ * with_base is copied into desc->with_base. */
+KINHIP_API int kin_urdf_tree(const kin_urdf* u, int32_t with_base, kin_tree_desc* desc);
+KINHIP_API int kin_urdf_link_name(const kin_urdf* u, int32_t link_id, const char** name);
+KINHIP_API int kin_urdf_joint_name(const kin_urdf* u, int32_t joint_id, const char** name);
+/* find_link / find_joint (src/mechanism.jl:191-192); KIN_E_KEY if absent */
+KINHIP_API int kin_urdf_find_link(const kin_urdf* u, const char* name, int32_t* id);
+KINHIP_API int kin_urdf_find_joint(const kin_urdf* u, const char* name, int32_t* id);
+/* BoxMetaData of a link's collision geometry (src/load_urdf.jl:1-18).
+ * *has_box = 0 when the link has no box collision. */
+KINHIP_API int kin_urdf_link_box(const kin_urdf* u, int32_t link_id, int32_t* has_box,
+                                 double* extents3, double* origin16);
+
+/* ------------------------------------------------------------------------- */
+/* Plans: one staged, device-resident evaluation program per request          */
+/* ------------------------------------------------------------------------- */
+typedef struct kin_plan_desc {
+    int32_t dtype;               /* kin_dtype */
+    int32_t n_q;                 /* batch columns: set_joint_angles(m, joints, angles) */
+    const int32_t* q_joint_ids;
+    int32_t n_out;               /* get_transform(m, link) for each of these links */
+    const int32_t* out_link_ids;
+    int32_t jac_link_id;         /* get_jacobian!(m, link, joints, ...); 0 = none */
+    int32_t n_jac;
+    const int32_t* jac_joint_ids;
+    uint32_t jac_flags;          /* KIN_WITH_ROT | KIN_RPY_JAC | KIN_ZERO_FILL */
+} kin_plan_desc;
+
+typedef struct kin_plan kin_plan;
+
+/* Stages the tree for this request onto the current HIP device
+ * (synchronous; call outside stream capture). */
+KINHIP_API int kin_plan_create(const kin_model* m, const kin_plan_desc* desc, kin_plan** out);
+KINHIP_API int kin_plan_destroy(kin_plan* p);
+/* Number of batch columns q must hold, Jacobian rows and columns. */
+KINHIP_API int kin_plan_shape(const kin_plan* p, int32_t* n_qcols, int32_t* jac_rows, int32_t* jac_cols);
+
+/* Batched get_transform (+ get_jacobian!) for N configurations:
+ * src/algorithm.jl:1-21 and :83-106 with set_joint_angles per config.
+ * poses may be NULL when n_out == 0; jac may be NULL when the plan has no
+ * Jacobian.  Device pointers; async on stream. */
+KINHIP_API int kin_plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n,
+                            void* poses, int64_t ldp, void* jac, int64_t ldj, void* stream);
+
+/* One-shot conveniences with an internal per-model plan cache (the first call
+ * for a request stages it synchronously; later calls are async).
+ * kin_get_transform_batch: poses of n_out links.  kin_get_jacobian_batch: the
+ * Jacobian of link over jac joints (pose optional).  The q columns are the
+ * given joints (+ base). */
+KINHIP_API int kin_get_transform_batch(kin_model* m, int32_t dtype, int32_t n_q, const int32_t* q_joint_ids,
+                                       const void* q, int64_t ldq, int64_t n, int32_t n_out,
+                                       const int32_t* out_link_ids, void* poses, int64_t ldp, void* stream);
+KINHIP_API int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_id, int32_t n_joints,
+                                      const int32_t* joint_ids, uint32_t jac_flags, const void* q,
+                                      int64_t ldq, int64_t n, void* pose, int64_t ldp, void* jac,
+                                      int64_t ldj, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Inverse kinematics                                                          */
+/* ------------------------------------------------------------------------- */
+/* Damped-least-squares IK (build-defined batched replacement of the SLSQP loop
+ * of inverse_kinematics!, src/inverse_kinematics.jl:23-64; iterates unpinned,
+ * acceptance pinned by test/test_inverse_kinematics.jl:19-23).
+ * The plan must have a Jacobian whose joints equal its q joints (same order)
+ * and jac_flags without KIN_RPY_JAC; its jac link is the IK target link.
+ *   target : [12][ldt] target poses (3x4 column-major)
+ *   q      : [n_qcols][ldq] initial angles in, solution out (clamped to limits)
+ *   iters  : [n] int32 iterations used (== max_iters => not converged) or NULL
+ *   err    : [2][n] final |dp|, |rot err| (dtype) or NULL                       */
+typedef struct kin_ik_params {
+    int32_t max_iters;  /* e.g. 64 */
+    double lambda;      /* damping, e.g. 1e-2 */
+    double tol_pos;     /* |dp| tolerance, e.g. 1e-3 */
+    double tol_rot;     /* |axis-angle error| tolerance, e.g. 1e-3 */
+    double max_step;    /* max |dq|_inf per iteration, e.g. 0.5 */
+    int32_t with_rot;   /* 0: position only */
+} kin_ik_params;
+KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
+                                void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,
+                                void* stream);
+
+/* point_inverse_kinematics_nakamura (src/algorithm.jl:116-131), batched:
+ * 50 SR-inverse iterations, `.+ sr_weight` broadcast quirk reproduced.
+ * points: [3][ldpt]; q: [n_q][ldq] in/out.  Plan: Jacobian over its q joints,
+ * model without base. */
+KINHIP_API int kin_point_ik_nakamura_batch(const kin_plan* p, const void* points, int64_t ldpt, void* q,
+                                           int64_t ldq, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KINHIP_H */

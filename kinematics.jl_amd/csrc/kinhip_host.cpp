@@ -1,0 +1,874 @@
+// kinhip_host.cpp -- C-ABI of libkinhip.so: models (Mechanism trees), plan
+// staging (tree -> device program, kinhip_prog.h) and launches.
+//
+// Reference semantics restated here (host side):
+//   Mechanism / create_rptable / is_relevant   src/mechanism.jl:117-181, 277
+//   joint_transform (static parts, fp64)       src/mechanism.jl:90-103
+//   set_joint_angles column layout             src/mechanism.jl:223-231
+//   get_jacobian! column relevance / errors    src/algorithm.jl:83-106
+//   add_new_link                                src/mechanism.jl:238-267
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "kinhip.h"
+#include "kinhip_host.h"
+#include "kinhip_internal.h"
+
+namespace kinhip {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+namespace {
+
+// rigid 3x4, row-major rotation
+struct M34 {
+    double r[9];
+    double t[3];
+};
+
+M34 m_identity() {
+    M34 m{};
+    m.r[0] = m.r[4] = m.r[8] = 1.0;
+    return m;
+}
+
+bool m_is_identity(const M34& m) {
+    const M34 I = m_identity();
+    return memcmp(&m, &I, sizeof(M34)) == 0;
+}
+
+M34 m_mul(const M34& a, const M34& b) {
+    M34 c;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j)
+            c.r[3 * i + j] = a.r[3 * i] * b.r[j] + a.r[3 * i + 1] * b.r[3 + j] + a.r[3 * i + 2] * b.r[6 + j];
+        c.t[i] = a.r[3 * i] * b.t[0] + a.r[3 * i + 1] * b.t[1] + a.r[3 * i + 2] * b.t[2] + a.t[i];
+    }
+    return c;
+}
+
+M34 m_from_col16(const double* T) {
+    M34 m;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) m.r[3 * i + j] = T[i + 4 * j];
+        m.t[i] = T[i + 12];
+    }
+    return m;
+}
+
+M34 m_rot_transpose(const M34& a) {  // inverse of a pure rotation
+    M34 m{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) m.r[3 * i + j] = a.r[3 * j + i];
+    return m;
+}
+
+// Rotations.jl UnitQuaternion(w, x, y, z) (normalising) -> RotMatrix
+M34 m_quat(double w, double x, double y, double z) {
+    const double n = sqrt(w * w + x * x + y * y + z * z);
+    w /= n; x /= n; y /= n; z /= n;
+    const double ww = w * w, xx = x * x, yy = y * y, zz = z * z;
+    const double xy = x * y, zw = w * z, xz = x * z, yw = y * w, yz = y * z, xw = w * x;
+    M34 m{};
+    m.r[0] = ww + xx - yy - zz; m.r[1] = 2 * (xy - zw);     m.r[2] = 2 * (xz + yw);
+    m.r[3] = 2 * (xy + zw);     m.r[4] = ww - xx + yy - zz; m.r[5] = 2 * (yz - xw);
+    m.r[6] = 2 * (xz - yw);     m.r[7] = 2 * (yz + xw);     m.r[8] = ww - xx - yy + zz;
+    return m;
+}
+
+template <typename T>
+void to_row12(const M34& m, T* out) {
+    for (int i = 0; i < 3; ++i) {
+        out[4 * i + 0] = (T)m.r[3 * i + 0];
+        out[4 * i + 1] = (T)m.r[3 * i + 1];
+        out[4 * i + 2] = (T)m.r[3 * i + 2];
+        out[4 * i + 3] = (T)m.t[i];
+    }
+}
+
+}  // namespace
+}  // namespace kinhip
+
+using namespace kinhip;
+
+struct kin_plan;
+
+struct kin_model {
+    int32_t n_links = 0;
+    std::vector<int32_t> jtype, jplink, jclink;  // 1-based link ids
+    std::vector<double> jpose;                    // [J][16] column-major
+    std::vector<double> jaxis;                    // [J][3]
+    std::vector<double> jlo, jhi;
+    std::vector<int32_t> link_pjoint;               // 0-based joint, -1 root
+    std::vector<std::vector<int32_t>> child_joints;  // per link, 0-based joints in joint order
+    std::vector<double> angles;                      // m.angles
+    bool with_base = false;
+    uint64_t version = 0;
+    std::mutex mu;
+    std::map<std::string, kin_plan*> cache;
+
+    int32_t n_joints() const { return (int32_t)jtype.size(); }
+    int32_t plink(int32_t l) const { return link_pjoint[l] < 0 ? -1 : jplink[link_pjoint[l]] - 1; }
+    M34 pose(int32_t j) const { return m_from_col16(&jpose[16 * j]); }
+    // joint motion at a constant angle (the right factor of joint_transform)
+    M34 motion_at(int32_t j, double a) const {
+        if (jtype[j] == KIN_JOINT_FIXED || a == 0.0) return m_identity();
+        const double* ax = &jaxis[3 * j];
+        if (jtype[j] == KIN_JOINT_REVOLUTE) {
+            const double s = sin(0.5 * a), c = cos(0.5 * a);
+            return m_quat(c, ax[0] * s, ax[1] * s, ax[2] * s);
+        }
+        M34 m = m_identity();
+        m.t[0] = ax[0] * a; m.t[1] = ax[1] * a; m.t[2] = ax[2] * a;
+        return m;
+    }
+    // joint_transform(joint, angle), src/mechanism.jl:90-103
+    M34 joint_tf(int32_t j, double a) const {
+        if (jtype[j] == KIN_JOINT_FIXED || a == 0.0) return pose(j);
+        return m_mul(pose(j), motion_at(j, a));
+    }
+    bool relevant(int32_t j, int32_t l) const {  // rptable[j][l]: l in subtree of j's child
+        const int32_t c = jclink[j] - 1;
+        for (int32_t x = l, guard = 0; x >= 0 && guard <= n_links; x = plink(x), ++guard)
+            if (x == c) return true;
+        return false;
+    }
+};
+
+struct kin_plan {
+    int32_t dtype = KIN_F32;
+    int32_t nqcols = 0, rows = 0, ncols = 0, n_q = 0, n_out = 0;
+    bool has_jac = false, with_base = false, has_rpy = false;
+    bool ik_ok = false;
+    std::string ik_why;
+    void* d_steps = nullptr;
+    KProg<float> pf{};
+    KProg<double> pd{};
+    LaunchGeom geom{256, 0, 8};
+    ~kin_plan() {
+        if (d_steps) (void)hipFree(d_steps);
+    }
+};
+
+namespace {
+
+int validate_tree(const kin_tree_desc* d) {
+    if (!d) return set_error(KIN_E_INVALID, "kin_model_create: null desc");
+    if (d->n_links < 1 || d->n_joints < 0) return set_error(KIN_E_INVALID, "kin_model_create: bad sizes");
+    if (d->n_joints > 0 && (!d->joint_type || !d->joint_plink || !d->joint_clink || !d->joint_pose || !d->joint_axis))
+        return set_error(KIN_E_INVALID, "kin_model_create: null joint arrays");
+    std::vector<int> parents(d->n_links, 0);
+    for (int32_t j = 0; j < d->n_joints; ++j) {
+        const int32_t t = d->joint_type[j];
+        if (t != KIN_JOINT_FIXED && t != KIN_JOINT_REVOLUTE && t != KIN_JOINT_PRISMATIC)
+            return set_error(KIN_E_INVALID, "kin_model_create: joint " + std::to_string(j + 1) + " has unknown type");
+        const int32_t p = d->joint_plink[j], c = d->joint_clink[j];
+        if (p < 1 || p > d->n_links || c < 1 || c > d->n_links)
+            return set_error(KIN_E_KEY, "kin_model_create: joint " + std::to_string(j + 1) + " link id out of range");
+        if (++parents[c - 1] > 1)
+            return set_error(KIN_E_INVALID, "kin_model_create: link " + std::to_string(c) + " has two parent joints");
+    }
+    return KIN_OK;
+}
+
+int finish_model(kin_model* m) {
+    const int32_t L = m->n_links, J = m->n_joints();
+    m->link_pjoint.assign(L, -1);
+    m->child_joints.assign(L, {});
+    for (int32_t j = 0; j < J; ++j) {
+        m->link_pjoint[m->jclink[j] - 1] = j;
+        m->child_joints[m->jplink[j] - 1].push_back(j);
+    }
+    for (int32_t l = 0; l < L; ++l) {  // cycle check
+        int32_t x = l, guard = 0;
+        while (x >= 0) {
+            if (++guard > L + 1) return set_error(KIN_E_INVALID, "kin_model_create: the joint graph has a cycle");
+            x = m->plink(x);
+        }
+    }
+    return KIN_OK;
+}
+
+// rotation A with A e_z = unit axis (exact for signed basis axes)
+M34 align_z(const double* a, double* scale) {
+    const double n = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    *scale = n;
+    if (n == 0.0) return m_identity();
+    const double z[3] = {a[0] / n, a[1] / n, a[2] / n};
+    if (z[0] == 0.0 && z[1] == 0.0 && z[2] == 1.0) return m_identity();
+    double h[3] = {0, 0, 1};
+    if (fabs(z[2]) >= 0.9) { h[0] = 1; h[2] = 0; }
+    double u[3] = {h[1] * z[2] - h[2] * z[1], h[2] * z[0] - h[0] * z[2], h[0] * z[1] - h[1] * z[0]};
+    const double un = sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    for (double& v : u) v /= un;
+    const double v[3] = {z[1] * u[2] - z[2] * u[1], z[2] * u[0] - z[0] * u[2], z[0] * u[1] - z[1] * u[0]};
+    M34 A{};
+    for (int i = 0; i < 3; ++i) {
+        A.r[3 * i + 0] = u[i];
+        A.r[3 * i + 1] = v[i];
+        A.r[3 * i + 2] = z[i];
+    }
+    return A;
+}
+
+struct SD {  // staged step, fp64
+    M34 F, X;
+    bool hasX = false;
+    double scale = 1, lo = -INFINITY, hi = INFINITY;
+    int32_t kind = MOT_NONE, jkind = MOT_NONE, qcol = -1, flags = 0, out = -1, load = LOAD_NONE, save = -1;
+    uint64_t colmask = 0;
+};
+
+struct Stager {
+    const kin_model& m;
+    const kin_plan_desc& d;
+    std::vector<int32_t> qcol;
+    std::vector<char> moving, rec, needed, node;
+    std::vector<uint64_t> colmask;
+    std::vector<std::vector<int32_t>> outs_of, cchildren;  // per link
+    std::vector<M34> Xinv;
+    std::vector<char> hasX;
+    std::vector<SD> steps;
+    uint64_t zmask = 0;
+    // LDS slots
+    std::vector<int> slot_of_link, slot_refs;
+    std::vector<int> free_slots;
+    int n_slots = 0;
+
+    Stager(const kin_model& m_, const kin_plan_desc& d_) : m(m_), d(d_) {}
+
+    int alloc_slot() {
+        if (!free_slots.empty()) {
+            int s = free_slots.back();
+            free_slots.pop_back();
+            return s;
+        }
+        slot_refs.push_back(0);
+        return n_slots++;
+    }
+    void consume(int slot) {
+        if (slot >= 0 && --slot_refs[slot] == 0) free_slots.push_back(slot);
+    }
+
+    int32_t cparent(int32_t v) const {  // nearest node ancestor (compressed parent), -1 for roots
+        for (int32_t x = m.plink(v); x >= 0; x = m.plink(x))
+            if (node[x]) return x;
+        return -1;
+    }
+
+    // edge u -> v (v a node); appends the edge step and duplicate-output steps
+    void emit_edge(int32_t v, int32_t load) {
+        SD st;
+        st.load = load;
+        std::vector<int32_t> path;  // joints from cparent(v) down to v
+        for (int32_t x = v; x >= 0 && !(x != v && node[x]); x = m.plink(x))
+            if (m.link_pjoint[x] >= 0) path.push_back(m.link_pjoint[x]);
+        const int32_t u = cparent(v);
+        if (u < 0 || path.empty()) {  // v is a root: pseudo-step on the root frame
+            st.F = m_identity();
+            Xinv[v] = m_identity();
+            hasX[v] = 0;
+        } else {
+            M34 S = hasX[u] ? Xinv[u] : m_identity();
+            for (size_t k = path.size() - 1; k >= 1; --k) S = m_mul(S, m.joint_tf(path[k], m.angles[path[k]]));
+            const int32_t jm = path[0];
+            if (moving[jm] || rec[jm]) {
+                double scale;
+                const M34 A = align_z(&m.jaxis[3 * jm], &scale);
+                st.F = m_mul(m_mul(S, m.pose(jm)), A);
+                st.scale = scale;
+                st.jkind = m.jtype[jm] == KIN_JOINT_PRISMATIC ? MOT_PRISM : MOT_REV;
+                st.lo = m.jlo[jm];
+                st.hi = m.jhi[jm];
+                if (rec[jm]) {
+                    st.flags |= SF_REC;
+                    st.colmask = colmask[jm];
+                }
+                if (moving[jm]) {
+                    st.kind = st.jkind;
+                    st.qcol = qcol[jm];
+                    if (st.kind == MOT_REV && scale != 1.0) st.flags |= SF_SCALE;
+                    Xinv[v] = m_rot_transpose(A);
+                } else {
+                    Xinv[v] = m_mul(m_rot_transpose(A), m.motion_at(jm, m.angles[jm]));
+                }
+                hasX[v] = !m_is_identity(Xinv[v]);
+            } else {
+                st.F = m_mul(S, m.joint_tf(jm, m.angles[jm]));
+                Xinv[v] = m_identity();
+                hasX[v] = 0;
+            }
+        }
+        st.X = Xinv[v];
+        st.hasX = hasX[v];
+        if (st.hasX) st.flags |= SF_HAS_X;
+        const auto& o = outs_of[v];
+        st.out = o.empty() ? -1 : o[0];
+        steps.push_back(st);
+        for (size_t k = 1; k < o.size(); ++k) {  // same link requested again: identity pseudo-steps
+            SD dup;
+            dup.F = m_identity();
+            dup.X = st.X;
+            dup.hasX = st.hasX;
+            dup.flags = st.hasX ? SF_HAS_X : 0;
+            dup.out = o[k];
+            steps.push_back(dup);
+        }
+    }
+
+    void emit_subtree(int32_t v, int32_t load) {
+        emit_edge(v, load);
+        const size_t edge_step = steps.size() - 1 - (outs_of[v].size() > 1 ? outs_of[v].size() - 1 : 0);
+        const auto& ch = cchildren[v];
+        if (ch.empty()) return;
+        int slot = -1;
+        if (ch.size() >= 2) {
+            slot = alloc_slot();
+            slot_refs[slot] = (int)ch.size() - 1;
+            steps[edge_step].save = slot;
+        }
+        emit_subtree(ch[0], LOAD_NONE);
+        for (size_t k = 1; k < ch.size(); ++k) {
+            emit_subtree_loaded(ch[k], slot);
+        }
+    }
+    void emit_subtree_loaded(int32_t v, int slot) {
+        emit_subtree(v, slot);
+        consume(slot);
+    }
+
+    int run(kin_plan& P) {
+        const int32_t L = m.n_links, J = m.n_joints();
+        if (d.dtype != KIN_F32 && d.dtype != KIN_F64) return set_error(KIN_E_INVALID, "plan: bad dtype");
+        if (d.n_q < 0 || d.n_out < 0 || d.n_jac < 0) return set_error(KIN_E_INVALID, "plan: negative count");
+        if ((d.n_q && !d.q_joint_ids) || (d.n_out && !d.out_link_ids) || (d.n_jac && !d.jac_joint_ids))
+            return set_error(KIN_E_INVALID, "plan: null id array");
+        qcol.assign(J, -1);
+        for (int32_t c = 0; c < d.n_q; ++c) {
+            const int32_t j = d.q_joint_ids[c] - 1;
+            if (j < 0 || j >= J) return set_error(KIN_E_KEY, "plan: q joint id " + std::to_string(j + 1) + " out of range");
+            qcol[j] = c;  // set_joint_angles: a repeated joint keeps the last value
+        }
+        moving.assign(J, 0);
+        for (int32_t j = 0; j < J; ++j) moving[j] = qcol[j] >= 0 && m.jtype[j] != KIN_JOINT_FIXED;
+        rec.assign(J, 0);
+        colmask.assign(J, 0);
+        const int32_t jl = d.jac_link_id - 1;
+        const bool has_jac = d.jac_link_id != 0;
+        if (has_jac) {
+            if (jl < 0 || jl >= L) return set_error(KIN_E_KEY, "plan: jac link id out of range");
+            if (d.n_jac > kMaxJacCols)
+                return set_error(KIN_E_UNSUPPORTED, "plan: more than 64 Jacobian columns");
+            for (int32_t c = 0; c < d.n_jac; ++c) {
+                const int32_t j = d.jac_joint_ids[c] - 1;
+                if (j < 0 || j >= J) return set_error(KIN_E_KEY, "plan: jac joint id out of range");
+                if (m.relevant(j, jl)) {
+                    if (m.jtype[j] == KIN_JOINT_FIXED)
+                        return set_error(KIN_E_METHOD, "MethodError: no joint_jacobian! method for fixed joint " +
+                                                           std::to_string(j + 1));
+                    rec[j] = 1;
+                    colmask[j] |= 1ull << c;
+                } else {
+                    zmask |= 1ull << c;
+                }
+            }
+        } else if (d.n_jac) {
+            return set_error(KIN_E_INVALID, "plan: Jacobian joints without a Jacobian link");
+        }
+        outs_of.assign(L, {});
+        for (int32_t o = 0; o < d.n_out; ++o) {
+            const int32_t l = d.out_link_ids[o] - 1;
+            if (l < 0 || l >= L) return set_error(KIN_E_KEY, "plan: output link id out of range");
+            outs_of[l].push_back(o);
+        }
+        needed.assign(L, 0);
+        auto mark = [&](int32_t l) {
+            for (int32_t x = l; x >= 0 && !needed[x]; x = m.plink(x)) needed[x] = 1;
+        };
+        for (int32_t o = 0; o < d.n_out; ++o) mark(d.out_link_ids[o] - 1);
+        if (has_jac) mark(jl);
+        // spine = the chain evaluated straight-line in registers (phase A): the
+        // Jacobian link, else the needed link with the most moving joints above it
+        int32_t spine = has_jac ? jl : -1;
+        if (!has_jac) {
+            int best = -1, best_depth = -1;
+            for (int32_t o = 0; o < d.n_out; ++o) {
+                const int32_t l = d.out_link_ids[o] - 1;
+                int mv = 0, depth = 0;
+                for (int32_t x = l; m.link_pjoint[x] >= 0; x = m.plink(x)) {
+                    mv += moving[m.link_pjoint[x]];
+                    ++depth;
+                }
+                if (mv > best || (mv == best && depth > best_depth)) {
+                    best = mv;
+                    best_depth = depth;
+                    spine = l;
+                }
+            }
+        }
+        // nodes: links whose frame is materialised (roots, children of moving or
+        // recorded joints, outputs, the spine); static branch points are folded
+        node.assign(L, 0);
+        for (int32_t l = 0; l < L; ++l) {
+            if (!needed[l]) continue;
+            const int32_t pj = m.link_pjoint[l];
+            node[l] = pj < 0 || moving[pj] || rec[pj] || !outs_of[l].empty() || l == spine;
+        }
+        // compressed children in tree (joint) order
+        cchildren.assign(L, {});
+        std::vector<int32_t> roots;
+        for (int32_t l = 0; l < L; ++l)
+            if (needed[l] && m.link_pjoint[l] < 0) roots.push_back(l);
+        for (int32_t r : roots) {
+            std::vector<std::pair<int32_t, int32_t>> work{{r, -1}};  // (link, nearest node ancestor)
+            while (!work.empty()) {
+                auto [x, anc] = work.back();
+                work.pop_back();
+                if (node[x] && anc >= 0) cchildren[anc].push_back(x);
+                const int32_t a2 = node[x] ? x : anc;
+                const auto& cj = m.child_joints[x];
+                for (auto it = cj.rbegin(); it != cj.rend(); ++it) {
+                    const int32_t c = m.jclink[*it] - 1;
+                    if (needed[c]) work.push_back({c, a2});
+                }
+            }
+        }
+        Xinv.assign(L, m_identity());
+        hasX.assign(L, 0);
+
+        // ---- phase A: root -> spine, straight-line, no loads ----
+        std::vector<std::pair<int32_t, int32_t>> pending;  // (child node, parent node)
+        int32_t sroot = -1;
+        int32_t nA = 0, spine_out = -1;
+        M34 Xl = m_identity();
+        int32_t lhx = 0;
+        slot_of_link.assign(L, -1);
+        if (spine >= 0) {
+            std::vector<int32_t> chain;  // nodes root..spine
+            for (int32_t x = spine; x >= 0; x = cparent(x)) chain.push_back(x);
+            std::reverse(chain.begin(), chain.end());
+            sroot = chain[0];
+            const size_t K = chain.size() - 1;
+            // a static last edge into a leaf spine folds into Xlast (no step)
+            bool fold = false;
+            if (K >= 1 && cchildren[spine].empty() && outs_of[spine].size() <= 1) {
+                const int32_t pj = m.link_pjoint[spine];
+                fold = !(moving[pj] || rec[pj]);
+            }
+            std::vector<int32_t> edge_step(chain.size(), -1);
+            for (size_t k = 0; k < chain.size(); ++k) {
+                const int32_t v = chain[k];
+                if (k == K && fold) {
+                    const int32_t u = chain[k - 1];
+                    Xl = hasX[u] ? Xinv[u] : m_identity();
+                    std::vector<int32_t> path;
+                    for (int32_t x = v; x != u; x = m.plink(x)) path.push_back(m.link_pjoint[x]);
+                    for (size_t p = path.size(); p-- > 0;) Xl = m_mul(Xl, m.joint_tf(path[p], m.angles[path[p]]));
+                    lhx = !m_is_identity(Xl);
+                    spine_out = outs_of[v].empty() ? -1 : outs_of[v][0];
+                } else if (k > 0 || !outs_of[v].empty()) {
+                    edge_step[k] = (int32_t)steps.size();
+                    emit_edge(v, LOAD_NONE);
+                }
+                const int32_t next = k < K ? chain[k + 1] : -1;
+                for (int32_t c : cchildren[v])
+                    if (c != next) pending.push_back({c, v});
+            }
+            if (!fold) {
+                Xl = Xinv[spine];
+                lhx = hasX[spine];
+            }
+            nA = (int32_t)steps.size();
+            if (nA > kMaxChain)
+                return set_error(KIN_E_UNSUPPORTED, "plan: root -> spine chain has " + std::to_string(nA) +
+                                                        " steps (max " + std::to_string(kMaxChain) + ")");
+            // slots for chain nodes with pending children (the root frame needs none)
+            std::map<int32_t, int> cnt;
+            for (auto& pc : pending) cnt[pc.second]++;
+            for (size_t k = 0; k < chain.size(); ++k) {
+                const int32_t v = chain[k];
+                auto it = cnt.find(v);
+                if (it == cnt.end() || v == sroot) continue;
+                const int s = alloc_slot();
+                slot_refs[s] = it->second;
+                slot_of_link[v] = s;
+                steps[edge_step[k]].save = s;
+            }
+            // pad to the compiled chain bound with identity steps
+            const int32_t bound = pick_chain_bound(nA);
+            while ((int32_t)steps.size() < bound) {
+                SD pad;
+                pad.F = m_identity();
+                pad.X = m_identity();
+                pad.scale = 0.0;
+                steps.push_back(pad);
+            }
+            nA = bound;
+        }
+        // ---- phase B ----
+        for (auto& pc : pending) {
+            const int32_t v = pc.first, u = pc.second;
+            if (u == sroot) {
+                emit_subtree(v, LOAD_ROOT);
+            } else {
+                const int s = slot_of_link[u];
+                emit_subtree(v, s);
+                consume(s);
+            }
+        }
+        for (int32_t r : roots) {
+            if (r == sroot) continue;
+            if (!outs_of[r].empty()) emit_edge(r, LOAD_ROOT);
+            for (int32_t c : cchildren[r]) emit_subtree(c, LOAD_ROOT);
+        }
+        if (n_slots > kMaxSlots)
+            return set_error(KIN_E_UNSUPPORTED, "plan: needs " + std::to_string(n_slots) + " LDS branch slots (max 8)");
+
+        // ---- finalize ----
+        P.dtype = d.dtype;
+        P.with_base = m.with_base;
+        P.n_q = d.n_q;
+        P.n_out = d.n_out;
+        P.nqcols = d.n_q + (m.with_base ? 3 : 0);
+        P.has_jac = has_jac;
+        P.rows = (d.jac_flags & KIN_WITH_ROT) ? 6 : 3;
+        P.ncols = has_jac ? d.n_jac + (m.with_base ? 3 : 0) : 0;
+        P.has_rpy = (d.jac_flags & KIN_RPY_JAC) != 0;
+        int32_t pflags = 0;
+        if (has_jac) pflags |= PF_JAC;
+        if (d.jac_flags & KIN_WITH_ROT) pflags |= PF_WITH_ROT;
+        if (d.jac_flags & KIN_RPY_JAC) pflags |= PF_RPY;
+        if (d.jac_flags & KIN_ZERO_FILL) pflags |= PF_ZERO;
+        if (m.with_base) pflags |= PF_BASE;
+        const size_t esz = d.dtype == KIN_F32 ? sizeof(float) : sizeof(double);
+        int block = 256;
+        while (block > 64 && (size_t)n_slots * 12 * block * esz > 64 * 1024) block /= 2;
+        P.geom.block = block;
+        P.geom.lds = (size_t)n_slots * 12 * block * esz;
+        P.geom.maxA = nA;
+        auto fill = [&](auto& K, auto* host) {
+            using T = std::remove_reference_t<decltype(host[0].F[0])>;
+            K.nA = nA;
+            K.nS = (int32_t)steps.size();
+            K.n_slots = n_slots;
+            K.rows = P.rows;
+            K.n_jac = d.n_jac;
+            K.flags = pflags;
+            K.base_col = d.n_q;
+            K.last_has_x = lhx;
+            K.spine_out = spine_out;
+            K.zmask = zmask;
+            to_row12<T>(Xl, K.Xlast);
+            for (size_t s = 0; s < steps.size(); ++s) {
+                const SD& a = steps[s];
+                auto& b = host[s];
+                memset(&b, 0, sizeof(b));
+                to_row12<T>(a.F, b.F);
+                to_row12<T>(a.X, b.X);
+                b.scale = (T)a.scale;
+                b.lo = (T)a.lo;
+                b.hi = (T)a.hi;
+                b.kind = a.kind;
+                b.jkind = a.jkind;
+                b.qcol = a.qcol;
+                b.flags = a.flags;
+                b.out = a.out;
+                b.load = a.load;
+                b.save = a.save;
+                b.colmask = a.colmask;
+            }
+        };
+        size_t bytes;
+        std::vector<unsigned char> host;
+        if (d.dtype == KIN_F32) {
+            bytes = std::max<size_t>(1, steps.size()) * sizeof(KStep<float>);
+            host.assign(bytes, 0);
+            fill(P.pf, reinterpret_cast<KStep<float>*>(host.data()));
+        } else {
+            bytes = std::max<size_t>(1, steps.size()) * sizeof(KStep<double>);
+            host.assign(bytes, 0);
+            fill(P.pd, reinterpret_cast<KStep<double>*>(host.data()));
+        }
+        hipError_t e = hipMalloc(&P.d_steps, bytes);
+        if (e != hipSuccess) {
+            P.d_steps = nullptr;
+            return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        e = hipMemcpy(P.d_steps, host.data(), bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+
+        // IK eligibility: Jacobian joints == q joints (same order, no repeats), no rpy rows
+        P.ik_ok = has_jac && d.n_jac == d.n_q && !(d.jac_flags & KIN_RPY_JAC);
+        if (P.ik_ok) {
+            std::vector<char> seen(J, 0);
+            for (int32_t c = 0; c < d.n_q; ++c) {
+                if (d.q_joint_ids[c] != d.jac_joint_ids[c]) { P.ik_ok = false; P.ik_why = "jac joints != q joints"; }
+                if (seen[d.q_joint_ids[c] - 1]++) { P.ik_ok = false; P.ik_why = "repeated joint"; }
+            }
+        } else {
+            P.ik_why = "IK needs a Jacobian over the q joints without rpy rows";
+        }
+        return KIN_OK;
+    }
+};
+
+int plan_create(const kin_model* m, const kin_plan_desc* d, kin_plan** out) {
+    if (!m || !d || !out) return set_error(KIN_E_INVALID, "kin_plan_create: null argument");
+    auto P = std::make_unique<kin_plan>();
+    Stager s(*m, *d);
+    const int rc = s.run(*P);
+    if (rc != KIN_OK) return rc;
+    *out = P.release();
+    return KIN_OK;
+}
+
+bool dev_ptr_ok(const void* p) { return p != nullptr; }
+
+std::string cache_key(const kin_model* m, const kin_plan_desc& d) {
+    std::ostringstream k;
+    k << m->version << '|' << d.dtype << '|' << d.jac_link_id << '|' << d.jac_flags << "|q";
+    for (int32_t c = 0; c < d.n_q; ++c) k << ',' << d.q_joint_ids[c];
+    k << "|o";
+    for (int32_t c = 0; c < d.n_out; ++c) k << ',' << d.out_link_ids[c];
+    k << "|j";
+    for (int32_t c = 0; c < d.n_jac; ++c) k << ',' << d.jac_joint_ids[c];
+    return k.str();
+}
+
+int cached_plan(kin_model* m, const kin_plan_desc& d, kin_plan** out) {
+    const std::string key = cache_key(m, d);
+    std::lock_guard<std::mutex> g(m->mu);
+    auto it = m->cache.find(key);
+    if (it != m->cache.end()) {
+        *out = it->second;
+        return KIN_OK;
+    }
+    kin_plan* p = nullptr;
+    const int rc = plan_create(m, &d, &p);
+    if (rc != KIN_OK) return rc;
+    m->cache[key] = p;
+    *out = p;
+    return KIN_OK;
+}
+
+void clear_cache(kin_model* m) {
+    std::lock_guard<std::mutex> g(m->mu);
+    for (auto& kv : m->cache) delete kv.second;
+    m->cache.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+int kin_abi_version(void) { return KINHIP_ABI_VERSION; }
+
+const char* kin_last_error(void) { return g_err.c_str(); }
+
+int kin_limits(int32_t* max_chain, int32_t* max_jac_cols, int32_t* max_slots) {
+    if (max_chain) *max_chain = kMaxChain;
+    if (max_jac_cols) *max_jac_cols = kMaxJacCols;
+    if (max_slots) *max_slots = kMaxSlots;
+    return KIN_OK;
+}
+
+int kin_model_create(const kin_tree_desc* d, kin_model** out) {
+    if (!out) return set_error(KIN_E_INVALID, "kin_model_create: null out");
+    int rc = validate_tree(d);
+    if (rc != KIN_OK) return rc;
+    auto m = std::make_unique<kin_model>();
+    const int32_t J = d->n_joints;
+    m->n_links = d->n_links;
+    m->jtype.assign(d->joint_type, d->joint_type + J);
+    m->jplink.assign(d->joint_plink, d->joint_plink + J);
+    m->jclink.assign(d->joint_clink, d->joint_clink + J);
+    m->jpose.assign(d->joint_pose, d->joint_pose + 16 * (size_t)J);
+    m->jaxis.assign(d->joint_axis, d->joint_axis + 3 * (size_t)J);
+    m->jlo.resize(J);
+    m->jhi.resize(J);
+    for (int32_t j = 0; j < J; ++j) {
+        m->jlo[j] = d->joint_lower ? d->joint_lower[j] : -INFINITY;
+        m->jhi[j] = d->joint_upper ? d->joint_upper[j] : INFINITY;
+    }
+    m->angles.assign(J, 0.0);
+    m->with_base = d->with_base != 0;
+    rc = finish_model(m.get());
+    if (rc != KIN_OK) return rc;
+    *out = m.release();
+    return KIN_OK;
+}
+
+int kin_model_destroy(kin_model* m) {
+    if (!m) return KIN_OK;
+    clear_cache(m);
+    delete m;
+    return KIN_OK;
+}
+
+int kin_model_num_links(const kin_model* m, int32_t* out) {
+    if (!m || !out) return set_error(KIN_E_INVALID, "null argument");
+    *out = m->n_links;
+    return KIN_OK;
+}
+
+int kin_model_num_joints(const kin_model* m, int32_t* out) {
+    if (!m || !out) return set_error(KIN_E_INVALID, "null argument");
+    *out = m->n_joints();
+    return KIN_OK;
+}
+
+int kin_model_set_angles(kin_model* m, const double* angles) {
+    if (!m) return set_error(KIN_E_INVALID, "null model");
+    if (angles) m->angles.assign(angles, angles + m->n_joints());
+    else m->angles.assign(m->n_joints(), 0.0);
+    clear_cache(m);
+    m->version++;
+    return KIN_OK;
+}
+
+int kin_model_is_relevant(const kin_model* m, int32_t joint_id, int32_t link_id, int32_t* out) {
+    if (!m || !out) return set_error(KIN_E_INVALID, "null argument");
+    if (joint_id < 1 || joint_id > m->n_joints()) return set_error(KIN_E_KEY, "joint id out of range");
+    if (link_id < 1 || link_id > m->n_links) return set_error(KIN_E_KEY, "link id out of range");
+    *out = m->relevant(joint_id - 1, link_id - 1) ? 1 : 0;
+    return KIN_OK;
+}
+
+int kin_model_add_link(kin_model* m, int32_t parent, const double* pose16, int32_t* new_id) {
+    if (!m || !pose16) return set_error(KIN_E_INVALID, "null argument");
+    if (parent < 1 || parent > m->n_links) return set_error(KIN_E_KEY, "parent link id out of range");
+    m->n_links += 1;
+    m->jtype.push_back(KIN_JOINT_FIXED);
+    m->jplink.push_back(parent);
+    m->jclink.push_back(m->n_links);
+    m->jpose.insert(m->jpose.end(), pose16, pose16 + 16);
+    const double ax[3] = {1, 0, 0};
+    m->jaxis.insert(m->jaxis.end(), ax, ax + 3);
+    m->jlo.push_back(-INFINITY);
+    m->jhi.push_back(INFINITY);
+    m->angles.push_back(0.0);
+    const int rc = finish_model(m);
+    if (rc != KIN_OK) return rc;
+    clear_cache(m);
+    m->version++;
+    if (new_id) *new_id = m->n_links;
+    return KIN_OK;
+}
+
+int kin_plan_create(const kin_model* m, const kin_plan_desc* d, kin_plan** out) { return plan_create(m, d, out); }
+
+int kin_plan_destroy(kin_plan* p) {
+    delete p;
+    return KIN_OK;
+}
+
+int kin_plan_shape(const kin_plan* p, int32_t* nq, int32_t* rows, int32_t* cols) {
+    if (!p) return set_error(KIN_E_INVALID, "null plan");
+    if (nq) *nq = p->nqcols;
+    if (rows) *rows = p->has_jac ? p->rows : 0;
+    if (cols) *cols = p->ncols;
+    return KIN_OK;
+}
+
+int kin_plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* poses, int64_t ldp, void* jac,
+                 int64_t ldj, void* stream) {
+    if (!p) return set_error(KIN_E_INVALID, "kin_plan_run: null plan");
+    if (n < 0) return set_error(KIN_E_INVALID, "kin_plan_run: n < 0");
+    if (n == 0) return KIN_OK;
+    if (p->nqcols > 0 && (!dev_ptr_ok(q) || ldq < n)) return set_error(KIN_E_INVALID, "kin_plan_run: bad q / ldq");
+    if (p->n_out > 0 && !poses) return set_error(KIN_E_INVALID, "kin_plan_run: null poses");
+    if (poses && ldp < n) return set_error(KIN_E_INVALID, "kin_plan_run: ldp < n");
+    if (p->has_jac && (!jac || ldj < n)) return set_error(KIN_E_INVALID, "kin_plan_run: bad jac / ldj");
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_fk<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)q, ldq, n, (float*)poses,
+                             ldp, (float*)jac, ldj, (hipStream_t)stream);
+    else
+        e = launch_fk<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)q, ldq, n,
+                              (double*)poses, ldp, (double*)jac, ldj, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_fk launch: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+
+int kin_get_transform_batch(kin_model* m, int32_t dtype, int32_t n_q, const int32_t* qids, const void* q,
+                            int64_t ldq, int64_t n, int32_t n_out, const int32_t* out_ids, void* poses, int64_t ldp,
+                            void* stream) {
+    if (!m) return set_error(KIN_E_INVALID, "null model");
+    kin_plan_desc d{dtype, n_q, qids, n_out, out_ids, 0, 0, nullptr, 0};
+    kin_plan* p;
+    const int rc = cached_plan(m, d, &p);
+    if (rc != KIN_OK) return rc;
+    if (n_out > 0 && !poses) return set_error(KIN_E_INVALID, "null poses");
+    return kin_plan_run(p, q, ldq, n, poses, ldp, nullptr, 0, stream);
+}
+
+int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_id, int32_t n_joints, const int32_t* jids,
+                           uint32_t flags, const void* q, int64_t ldq, int64_t n, void* pose, int64_t ldp, void* jac,
+                           int64_t ldj, void* stream) {
+    if (!m) return set_error(KIN_E_INVALID, "null model");
+    if (link_id == 0) return set_error(KIN_E_KEY, "link id 0");
+    const int32_t out_ids[1] = {link_id};
+    kin_plan_desc d{dtype, n_joints, jids, pose ? 1 : 0, out_ids, link_id, n_joints, jids, flags};
+    kin_plan* p;
+    const int rc = cached_plan(m, d, &p);
+    if (rc != KIN_OK) return rc;
+    return kin_plan_run(p, q, ldq, n, pose, ldp, jac, ldj, stream);
+}
+
+int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, void* q,
+                     int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
+    if (!p || !prm) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: null argument");
+    if (!p->ik_ok) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: plan not usable for IK: " + p->ik_why);
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
+    if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0))
+        return set_error(KIN_E_INVALID, "bad IK parameters");
+    IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot};
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,
+                                 (float*)q, ldq, n, iters, (float*)err, lde, (hipStream_t)stream);
+    else
+        e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
+                                  (double*)q, ldq, n, iters, (double*)err, lde, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+
+int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt, void* q, int64_t ldq, int64_t n,
+                                void* stream) {
+    if (!p) return set_error(KIN_E_INVALID, "null plan");
+    if (!p->ik_ok || p->with_base)
+        return set_error(KIN_E_INVALID, "kin_point_ik_nakamura_batch: plan needs jac joints == q joints, no base");
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if (!pts || ldpt < n || !q || ldq < n) return set_error(KIN_E_INVALID, "bad pointer / stride");
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_nakamura<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)pts, ldpt,
+                                   (float*)q, ldq, n, (hipStream_t)stream);
+    else
+        e = launch_nakamura<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)pts, ldpt,
+                                    (double*)q, ldq, n, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_nakamura launch: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+
+}  // extern "C"

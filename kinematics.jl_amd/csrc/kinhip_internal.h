@@ -1,0 +1,37 @@
+// kinhip_internal.h -- host-side launch entry points of the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kinhip_prog.h"
+
+namespace kinhip {
+
+// phase-A chain bounds compiled into the kernels (kinhip_kernels.hip)
+inline int pick_chain_bound(int n) { return n <= 4 ? 4 : n <= 8 ? 8 : n <= 12 ? 12 : n <= 16 ? 16 : 32; }
+
+struct LaunchGeom {
+    int block;      // threads per workgroup (multiple of 64)
+    size_t lds;     // dynamic LDS bytes
+    int maxA;       // phase-A steps as compiled (4 / 8 / 12 / 16 / 32); the program is padded to it
+};
+
+template <typename T>
+hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, hipStream_t st);
+
+struct IkArgs {
+    int32_t max_iters;
+    double lambda, tol_pos, tol_rot, max_step;
+    int32_t with_rot;
+};
+
+template <typename T>
+hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
+                         const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
+                         int64_t lde, hipStream_t st);
+
+template <typename T>
+hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
+                           int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st);
+
+}  // namespace kinhip

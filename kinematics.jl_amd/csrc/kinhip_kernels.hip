@@ -1,0 +1,733 @@
+// kinhip_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the batched
+// kinematics engine.  Compiled only for --offload-arch=gfx950.
+//
+// Reference semantics (HiroIshida/Kinematics.jl):
+//   k_fk        get_transform over many links + get_jacobian!  (src/algorithm.jl:1-106,
+//               joint_transform src/mechanism.jl:90-103, rpy src/transform.jl:45-48)
+//   k_ik_dls    batched damped-least-squares replacement of the SLSQP loop of
+//               inverse_kinematics! (src/inverse_kinematics.jl:23-64), build-defined
+//   k_nakamura  point_inverse_kinematics_nakamura (src/algorithm.jl:116-131)
+//
+// Execution model: one configuration per lane (wave64).  Joint angles, poses
+// and Jacobians are SoA with the configuration index fastest, so every load
+// and store of a wave touches 64 consecutive elements (256 B fp32 / 512 B
+// fp64).  The staged program (kinhip_prog.h) is identical for every lane: its
+// fields are read with uniform addresses (scalar loads through the scalar
+// cache), and its control flow is wave-uniform.  The root -> Jacobian-link
+// chain ("phase A", <= MAXA steps) is fully unrolled so that the per-joint
+// world origins/axes the Jacobian needs stay in registers; other links are
+// evaluated by a uniform loop that branches through per-lane LDS slots.
+// No MFMA: 3x4 rigid products are not a dense contraction; the kernels are
+// HBM-bound at the sizes of BASELINE.json (roofline).
+#include <hip/hip_runtime.h>
+
+#include "kinhip_internal.h"
+
+namespace kinhip {
+namespace {
+
+template <typename T>
+struct Fr {
+    T r[9];  // row-major rotation
+    T t[3];
+};
+
+// sin/cos of joint angles.  The library sincos carries a Payne-Hanek
+// reduction for huge arguments that, inlined once per joint, dominates the
+// kernel's code and register budget.  Joint angles are small, so: Cody-Waite
+// reduction by pi/2 with FMA-split constants, minimax kernels on [-pi/4, pi/4]
+// (Cephes sinf/cosf for fp32, fdlibm __kernel_sin/__kernel_cos for fp64), and
+// the library call kept only behind a rarely taken |x| bound.
+__device__ __noinline__ void sincos_slow(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __noinline__ void sincos_slow(double x, double* s, double* c) { sincos(x, s, c); }
+
+__device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
+    if (__builtin_expect(!(fabsf(x) < 8192.0f), 0)) {
+        sincos_slow(x, s, c);
+        return;
+    }
+    const float j = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-j, 1.57079637050628662109375f, x);
+    r = fmaf(-j, -4.37113900018624283e-8f, r);
+    const float z = r * r;
+    const float sp = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float cp = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                          fmaf(-0.5f, z, 1.0f));
+    const int qd = (int)j & 3;
+    const float ss = (qd & 1) ? cp : sp, cc = (qd & 1) ? sp : cp;
+    *s = (qd & 2) ? -ss : ss;
+    *c = ((qd + 1) & 2) ? -cc : cc;
+}
+
+__device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
+    if (__builtin_expect(!(fabs(x) < 1048576.0), 0)) {
+        sincos_slow(x, s, c);
+        return;
+    }
+    const double j = rint(x * 0.63661977236758134308);
+    double r = fma(-j, 1.57079632679489655800e+00, x);
+    r = fma(-j, 6.12323399573676603587e-17, r);
+    r = fma(-j, -1.49738490485916983e-33, r);
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                                  2.75573137070700676789e-06),
+                                        -1.98412698298579493134e-04),
+                              8.33333333332248946124e-03),
+                          -1.66666666666666324348e-01);
+    const double sp = fma(r * z, ps, r);
+    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                   -2.75573143513906633035e-07),
+                                         2.48015872894767294178e-05),
+                               -1.38888888888741095749e-03),
+                           4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cp = w + (((1.0 - w) - hz) + z * pc);
+    const int qd = (int)(long long)j & 3;
+    const double ss = (qd & 1) ? cp : sp, cc = (qd & 1) ? sp : cp;
+    *s = (qd & 2) ? -ss : ss;
+    *c = ((qd + 1) & 2) ? -cc : cc;
+}
+__device__ __forceinline__ float atan2_t(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double atan2_t(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float sqrt_t(float x) { return sqrtf(x); }
+__device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
+
+template <typename T>
+__device__ __forceinline__ void set_identity(Fr<T>& f) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f.r[k] = (k % 4 == 0) ? T(1) : T(0);
+    f.t[0] = f.t[1] = f.t[2] = T(0);
+}
+
+// f <- f * F   (F: row-major 3x4 in uniform memory)
+template <typename T>
+__device__ __forceinline__ void mul_rigid(Fr<T>& f, const T* __restrict__ F) {
+    const T F0 = F[0], F1 = F[1], F2 = F[2], F3 = F[3];
+    const T F4 = F[4], F5 = F[5], F6 = F[6], F7 = F[7];
+    const T F8 = F[8], F9 = F[9], F10 = F[10], F11 = F[11];
+    Fr<T> g;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
+        g.r[3 * i + 0] = fma(a, F0, fma(b, F4, c * F8));
+        g.r[3 * i + 1] = fma(a, F1, fma(b, F5, c * F9));
+        g.r[3 * i + 2] = fma(a, F2, fma(b, F6, c * F10));
+        g.t[i] = fma(a, F3, fma(b, F7, fma(c, F11, f.t[i])));
+    }
+    f = g;
+}
+
+template <typename T>
+__device__ __forceinline__ void mul_rigid_regs(Fr<T>& out, const Fr<T>& f, const T (&F)[12]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
+        out.r[3 * i + 0] = fma(a, F[0], fma(b, F[4], c * F[8]));
+        out.r[3 * i + 1] = fma(a, F[1], fma(b, F[5], c * F[9]));
+        out.r[3 * i + 2] = fma(a, F[2], fma(b, F[6], c * F[10]));
+        out.t[i] = fma(a, F[3], fma(b, F[7], fma(c, F[11], f.t[i])));
+    }
+}
+
+// joint motion in the canonical frame (axis = local z), branch-free in the
+// joint kind: revolute -> (c, s, 0), prismatic -> (1, 0, scale*q), none -> (1, 0, 0)
+template <typename T>
+__device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T scale, T qv) {
+    const bool rev = kind == MOT_REV;
+    T th = rev ? qv : T(0);
+    if (flags & SF_SCALE) {  // UnitQuaternion normalisation of a non-unit axis
+        T sh, ch;
+        sincos_t(T(0.5) * qv, &sh, &ch);
+        th = T(2) * atan2_t(scale * sh, ch);
+    }
+    T s, c;
+    sincos_t(th, &s, &c);
+    const T d = (kind == MOT_PRISM) ? scale * qv : T(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1];
+        f.r[3 * i] = fma(a, c, b * s);
+        f.r[3 * i + 1] = fma(b, c, -(a * s));
+        f.t[i] = fma(f.r[3 * i + 2], d, f.t[i]);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void base_frame(Fr<T>& f, T bx, T by, T th) {  // src/transform.jl:33-37
+    set_identity(f);
+    T s, c;
+    sincos_t(th, &s, &c);
+    f.r[0] = c; f.r[1] = -s;
+    f.r[3] = s; f.r[4] = c;
+    f.t[0] = bx; f.t[1] = by;
+}
+
+// 3x4 column-major SoA store (k = row + 3*col)
+template <typename T>
+__device__ __forceinline__ void store_pose(T* __restrict__ dst, int64_t ld, const Fr<T>& L) {
+    dst[0 * ld] = L.r[0]; dst[1 * ld] = L.r[3]; dst[2 * ld] = L.r[6];
+    dst[3 * ld] = L.r[1]; dst[4 * ld] = L.r[4]; dst[5 * ld] = L.r[7];
+    dst[6 * ld] = L.r[2]; dst[7 * ld] = L.r[5]; dst[8 * ld] = L.r[8];
+    dst[9 * ld] = L.t[0]; dst[10 * ld] = L.t[1]; dst[11 * ld] = L.t[2];
+}
+
+template <typename T>
+__device__ __forceinline__ void link_frame(Fr<T>& L, const Fr<T>& C, bool has_x, const T* __restrict__ X) {
+    if (has_x) {
+        T Xr[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Xr[k] = X[k];
+        mul_rigid_regs(L, C, Xr);
+    } else {
+        L = C;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void slot_store(T* slots, int slot, int B, int tid, const Fr<T>& f) {
+    T* s = slots + (size_t)slot * 12 * B + tid;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s[k * B] = f.r[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[(9 + k) * B] = f.t[k];
+}
+
+template <typename T>
+__device__ __forceinline__ void slot_load(const T* slots, int slot, int B, int tid, Fr<T>& f) {
+    const T* s = slots + (size_t)slot * 12 * B + tid;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f.r[k] = s[k * B];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.t[k] = s[(9 + k) * B];
+}
+
+// One phase-A step: C <- C F; record (o, z); motion.  Straight-line: padded
+// steps are identities with scale 0, so records and motion need no branch.
+template <typename T>
+__device__ __forceinline__ void step_a(Fr<T>& f, const KStep<T>& st, T qv, T (&o)[3], T (&z)[3]) {
+    mul_rigid(f, st.F);
+    o[0] = f.t[0]; o[1] = f.t[1]; o[2] = f.t[2];  // _get_joint_axis, src/algorithm.jl:42-54
+    const T sc = st.scale;
+    z[0] = f.r[2] * sc; z[1] = f.r[5] * sc; z[2] = f.r[8] * sc;
+    motion(f, st.kind, st.flags, sc, qv);
+}
+
+// --------------------------------------------------------------------------
+// k_fk: batched get_transform (any set of links) + get_jacobian! of one link
+// --------------------------------------------------------------------------
+template <typename T, int MAXA>
+__global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __restrict__ S,
+                                            const T* __restrict__ q, int64_t ldq, int64_t n,
+                                            T* __restrict__ poses, int64_t ldp, T* __restrict__ jac,
+                                            int64_t ldj) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* slots = reinterpret_cast<T*>(smem);
+    const int B = blockDim.x, tid = threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * B + tid;
+    if (i >= n) return;  // no block-wide barrier below: LDS slots are per lane
+
+    const bool base = (P.flags & PF_BASE) != 0;
+    T bx = T(0), by = T(0), bth = T(0);
+    if (base) {
+        bx = q[(int64_t)P.base_col * ldq + i];
+        by = q[(int64_t)(P.base_col + 1) * ldq + i];
+        bth = q[(int64_t)(P.base_col + 2) * ldq + i];
+    }
+    // every phase-A angle load issued up front (independent, coalesced)
+    T qa[MAXA];
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        qa[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+    }
+    Fr<T> root;
+    if (base) base_frame(root, bx, by, bth);
+    else set_identity(root);
+
+    Fr<T> f = root;
+    T ro[MAXA][3], rz[MAXA][3];
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const KStep<T>& st = S[s];
+        step_a(f, st, qa[s], ro[s], rz[s]);
+        if (st.out >= 0) {
+            Fr<T> L;
+            link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
+            store_pose(poses + (int64_t)st.out * 12 * ldp + i, ldp, L);
+        }
+        if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
+    }
+
+    if ((P.flags & PF_JAC) || P.spine_out >= 0) {
+        Fr<T> L;
+        link_frame(L, f, P.last_has_x != 0, P.Xlast);
+        if (P.spine_out >= 0) store_pose(poses + (int64_t)P.spine_out * 12 * ldp + i, ldp, L);
+        if (P.flags & PF_JAC) {
+            const T px = L.t[0], py = L.t[1], pz = L.t[2];
+            const int rows = P.rows;
+            const bool with_rot = (P.flags & PF_WITH_ROT) != 0;
+            const bool zero = (P.flags & PF_ZERO) != 0;
+            // rpy_derivative! coefficients (src/algorithm.jl:56-63) from RotZYX(L)
+            T k11 = 0, k12 = 0, k21 = 0, k22 = 0, k31 = 0, k32 = 0;
+            const bool rpy = with_rot && (P.flags & PF_RPY);
+            if (rpy) {
+                const T t1 = atan2_t(L.r[3], L.r[0]);
+                T st1, ct1;
+                sincos_t(t1, &st1, &ct1);
+                const T t2 = atan2_t(-L.r[6], fma(L.r[3], st1, L.r[0] * ct1));
+                T s2, c2, s3, c3;
+                sincos_t(-t2, &s2, &c2);
+                sincos_t(-t1, &s3, &c3);
+                k11 = c3 / c2; k12 = -(s3 / c2);
+                k21 = s3; k22 = c3;
+                k31 = -(c3 * s2 / c2); k32 = s3 * s2 / c2;
+            }
+#pragma unroll
+            for (int s = 0; s < MAXA; ++s) {
+                if (S[s].flags & SF_REC) {
+                    const T zx = rz[s][0], zy = rz[s][1], zz = rz[s][2];
+                    T lin[3], ang[3];
+                    const bool prism = S[s].jkind == MOT_PRISM;
+                    if (prism) {
+                        lin[0] = zx; lin[1] = zy; lin[2] = zz;
+                        ang[0] = ang[1] = ang[2] = T(0);
+                    } else {
+                        const T dx = px - ro[s][0], dy = py - ro[s][1], dz = pz - ro[s][2];
+                        lin[0] = fma(zy, dz, -(zz * dy));
+                        lin[1] = fma(zz, dx, -(zx * dz));
+                        lin[2] = fma(zx, dy, -(zy * dx));
+                        if (rpy) {
+                            ang[0] = fma(k11, zx, k12 * zy);
+                            ang[1] = fma(k21, zx, k22 * zy);
+                            ang[2] = fma(k31, zx, fma(k32, zy, zz));
+                        } else {
+                            ang[0] = zx; ang[1] = zy; ang[2] = zz;
+                        }
+                    }
+                    uint64_t m = S[s].colmask;
+                    while (m) {
+                        const int c = __builtin_ctzll(m);
+                        m &= m - 1;
+                        T* col = jac + (int64_t)c * rows * ldj + i;
+                        col[0] = lin[0]; col[ldj] = lin[1]; col[2 * ldj] = lin[2];
+                        if (with_rot && (!prism || zero)) {
+                            col[3 * ldj] = ang[0]; col[4 * ldj] = ang[1]; col[5 * ldj] = ang[2];
+                        }
+                    }
+                }
+            }
+            if (zero) {
+                uint64_t m = P.zmask;
+                while (m) {
+                    const int c = __builtin_ctzll(m);
+                    m &= m - 1;
+                    T* col = jac + (int64_t)c * rows * ldj + i;
+                    for (int r = 0; r < rows; ++r) col[r * ldj] = T(0);
+                }
+            }
+            if (base) {  // src/algorithm.jl:98-105
+                const T x = px - bx, y = py - by;
+                T* c0 = jac + (int64_t)P.n_jac * rows * ldj + i;
+                T* c1 = c0 + (int64_t)rows * ldj;
+                T* c2 = c1 + (int64_t)rows * ldj;
+                c0[0] = T(1); c0[ldj] = T(0); c0[2 * ldj] = T(0);
+                c1[0] = T(0); c1[ldj] = T(1); c1[2 * ldj] = T(0);
+                c2[0] = -y; c2[ldj] = x; c2[2 * ldj] = T(0);
+                if (with_rot) {
+                    c0[3 * ldj] = T(0); c0[4 * ldj] = T(0); c0[5 * ldj] = T(0);
+                    c1[3 * ldj] = T(0); c1[4 * ldj] = T(0); c1[5 * ldj] = T(0);
+                    c2[3 * ldj] = T(0); c2[4 * ldj] = T(0); c2[5 * ldj] = T(1);
+                }
+            }
+        }
+    }
+
+    // phase B: the remaining links (uniform loop, LDS slots at branch points)
+    for (int s = P.nA; s < P.nS; ++s) {
+        const KStep<T>& st = S[s];
+        const int32_t ld = st.load;
+        if (ld == LOAD_ROOT) f = root;
+        else if (ld >= 0) slot_load(slots, ld, B, tid, f);
+        mul_rigid(f, st.F);
+        if (st.kind != MOT_NONE) motion(f, st.kind, st.flags, st.scale, q[(int64_t)st.qcol * ldq + i]);
+        if (st.out >= 0) {
+            Fr<T> L;
+            link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
+            store_pose(poses + (int64_t)st.out * 12 * ldp + i, ldp, L);
+        }
+        if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
+    }
+}
+
+// --------------------------------------------------------------------------
+// shared phase-A evaluator for the IK kernels: q per step in registers
+// --------------------------------------------------------------------------
+template <typename T, int MAXA>
+__device__ __forceinline__ void chain_records(const KProg<T>& P, const KStep<T>* __restrict__ S,
+                                              const Fr<T>& root, const T (&qs)[MAXA], Fr<T>& L,
+                                              T (&ro)[MAXA][3], T (&rz)[MAXA][3]) {
+    Fr<T> f = root;
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) step_a(f, S[s], qs[s], ro[s], rz[s]);
+    link_frame(L, f, P.last_has_x != 0, P.Xlast);
+}
+
+// Jacobian column of phase-A step s (geometric; zero for non-recorded steps)
+template <typename T, int ROWS>
+__device__ __forceinline__ void jcol(const KStep<T>& st, const T (&o)[3], const T (&z)[3], const Fr<T>& L,
+                                     T (&J)[ROWS]) {
+    const T m = (st.flags & SF_REC) ? T(1) : T(0);
+    if (st.jkind == MOT_PRISM) {
+        J[0] = m * z[0]; J[1] = m * z[1]; J[2] = m * z[2];
+        if constexpr (ROWS == 6) { J[3] = T(0); J[4] = T(0); J[5] = T(0); }
+    } else {
+        const T dx = L.t[0] - o[0], dy = L.t[1] - o[1], dz = L.t[2] - o[2];
+        J[0] = m * fma(z[1], dz, -(z[2] * dy));
+        J[1] = m * fma(z[2], dx, -(z[0] * dz));
+        J[2] = m * fma(z[0], dy, -(z[1] * dx));
+        if constexpr (ROWS == 6) { J[3] = m * z[0]; J[4] = m * z[1]; J[5] = m * z[2]; }
+    }
+}
+
+// world rotation vector w with exp([w]) R = Rt  (log of Rt R^T)
+template <typename T>
+__device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (&w)[3]) {
+    T E[9];  // row-major E = Rt * R^T
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+            E[3 * a + b] = fma(Rt[3 * a], R[3 * b], fma(Rt[3 * a + 1], R[3 * b + 1], Rt[3 * a + 2] * R[3 * b + 2]));
+    const T v0 = T(0.5) * (E[7] - E[5]);
+    const T v1 = T(0.5) * (E[2] - E[6]);
+    const T v2 = T(0.5) * (E[3] - E[1]);
+    const T s = sqrt_t(v0 * v0 + v1 * v1 + v2 * v2);
+    const T c = T(0.5) * (E[0] + E[4] + E[8] - T(1));
+    const T th = atan2_t(s, c);
+    if (s > T(1e-7)) {
+        const T k = th / s;
+        w[0] = v0 * k; w[1] = v1 * k; w[2] = v2 * k;
+    } else if (c > T(0)) {
+        w[0] = v0; w[1] = v1; w[2] = v2;
+    } else {
+        int b = 0;
+        if (E[4] > E[0]) b = 1;
+        if (E[8] > E[4 * b]) b = 2;
+        T a[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) a[k] = T(0.5) * (E[3 * k + b] + E[3 * b + k]);
+        a[b] = T(0.5) * (E[4 * b] + T(1));
+        const T nn = sqrt_t(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w[k] = a[k] / nn * th;
+    }
+}
+
+template <typename T>
+struct IkArgsT {
+    int32_t max_iters;
+    T lam2, tol_pos, tol_rot, max_step;
+};
+
+// --------------------------------------------------------------------------
+// k_ik_dls: batched damped least squares, dq = J^T (J J^T + lambda^2 I)^-1 e
+// --------------------------------------------------------------------------
+template <typename T, int MAXA, int ROWS>
+__global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>* __restrict__ S,
+                                                const IkArgsT<T> a, const T* __restrict__ tgt, int64_t ldt,
+                                                T* __restrict__ q, int64_t ldq, int64_t n,
+                                                int32_t* __restrict__ iters, T* __restrict__ err,
+                                                int64_t lde) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    T Rt[9], pt[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Rt[3 * r + c] = tgt[(int64_t)(r + 3 * c) * ldt + i];
+        pt[r] = tgt[(int64_t)(9 + r) * ldt + i];
+    }
+    T qs[MAXA];
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        qs[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+    }
+    const bool base = (P.flags & PF_BASE) != 0;
+    T b[3] = {T(0), T(0), T(0)};
+    if (base)
+        for (int k = 0; k < 3; ++k) b[k] = q[(int64_t)(P.base_col + k) * ldq + i];
+
+    int it = 0;
+    T ep = 0, er = 0;
+    T ro[MAXA][3], rz[MAXA][3];
+    for (;; ++it) {
+        Fr<T> root, L;
+        if (base) base_frame(root, b[0], b[1], b[2]);
+        else set_identity(root);
+        chain_records<T, MAXA>(P, S, root, qs, L, ro, rz);
+        T e[6];
+        e[0] = pt[0] - L.t[0]; e[1] = pt[1] - L.t[1]; e[2] = pt[2] - L.t[2];
+        ep = sqrt_t(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        er = T(0);
+        if constexpr (ROWS == 6) {
+            T w[3];
+            rot_error(Rt, L.r, w);
+            e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
+            er = sqrt_t(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        }
+        if ((ep < a.tol_pos && er < a.tol_rot) || it >= a.max_iters) break;
+
+        T Jb[3][ROWS];
+        if (base) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) Jb[k][r] = T(0);
+            Jb[0][0] = T(1);
+            Jb[1][1] = T(1);
+            Jb[2][0] = -(L.t[1] - b[1]);
+            Jb[2][1] = L.t[0] - b[0];
+            if constexpr (ROWS == 6) Jb[2][5] = T(1);
+        }
+        // pass 0: every joint; pass 1 (lanes that need it): joints sitting on a
+        // limit that the step pushes further out get weight 0 and the system is
+        // re-solved (same rule as the oracle's or_ik_dls_batch)
+        T w[MAXA];
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) w[s] = T(1);
+        T dq[MAXA], db[3] = {T(0), T(0), T(0)};
+        T mx = T(0);
+        for (int pass = 0; pass < 2; ++pass) {
+            // A = J W J^T + lambda^2 I  (lower triangle)
+            T A[ROWS][ROWS];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? a.lam2 : T(0);
+#pragma unroll
+            for (int s = 0; s < MAXA; ++s) {
+                T J[ROWS];
+                jcol<T, ROWS>(S[s], ro[s], rz[s], L, J);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) J[r] *= w[s];
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                    for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+            }
+            if (base) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                        for (int c = 0; c <= r; ++c) A[r][c] = fma(Jb[k][r], Jb[k][c], A[r][c]);
+            }
+            // Cholesky A = L L^T (in place, lower), then y = A^-1 e
+#pragma unroll
+            for (int j = 0; j < ROWS; ++j) {
+                T d = A[j][j];
+#pragma unroll
+                for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
+                d = sqrt_t(d);
+                A[j][j] = d;
+#pragma unroll
+                for (int r = j + 1; r < ROWS; ++r) {
+                    T sm = A[r][j];
+#pragma unroll
+                    for (int k = 0; k < j; ++k) sm -= A[r][k] * A[j][k];
+                    A[r][j] = sm / d;
+                }
+            }
+            T y[ROWS];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                T sm = e[r];
+#pragma unroll
+                for (int k = 0; k < r; ++k) sm -= A[r][k] * y[k];
+                y[r] = sm / A[r][r];
+            }
+#pragma unroll
+            for (int r = ROWS - 1; r >= 0; --r) {
+                T sm = y[r];
+#pragma unroll
+                for (int k = r + 1; k < ROWS; ++k) sm -= A[k][r] * y[k];
+                y[r] = sm / A[r][r];
+            }
+            bool blocked = false;
+            mx = T(0);
+#pragma unroll
+            for (int s = 0; s < MAXA; ++s) {
+                T J[ROWS];
+                jcol<T, ROWS>(S[s], ro[s], rz[s], L, J);
+                T v = T(0);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
+                v *= w[s];
+                dq[s] = v;
+                if ((qs[s] <= S[s].lo && v < T(0)) || (qs[s] >= S[s].hi && v > T(0))) {
+                    blocked = true;
+                    w[s] = T(0);
+                }
+                mx = fmax(mx, fabs(v));
+            }
+            if (base) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    T v = T(0);
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r) v = fma(Jb[k][r], y[r], v);
+                    db[k] = v;
+                    mx = fmax(mx, fabs(v));
+                }
+            }
+            if (!blocked) break;
+        }
+        const T sc = mx > a.max_step ? a.max_step / mx : T(1);
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(qs[s] + sc * dq[s], S[s].lo), S[s].hi);
+        if (base)
+            for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
+    }
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        if (c >= 0) q[(int64_t)c * ldq + i] = qs[s];
+    }
+    if (base)
+        for (int k = 0; k < 3; ++k) q[(int64_t)(P.base_col + k) * ldq + i] = b[k];
+    if (iters) iters[i] = it;
+    if (err) {
+        err[i] = ep;
+        err[lde + i] = er;
+    }
+}
+
+// --------------------------------------------------------------------------
+// k_nakamura: point_inverse_kinematics_nakamura, 50 iterations
+// --------------------------------------------------------------------------
+template <typename T, int MAXA>
+__global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<T>* __restrict__ S,
+                                                  const T* __restrict__ pts, int64_t ldpt, T* __restrict__ q,
+                                                  int64_t ldq, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const T pd0 = pts[i], pd1 = pts[ldpt + i], pd2 = pts[2 * ldpt + i];
+    T qs[MAXA];
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        qs[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+    }
+    Fr<T> root;
+    set_identity(root);
+    T ro[MAXA][3], rz[MAXA][3];
+    for (int it = 0; it < 50; ++it) {
+        Fr<T> L;
+        chain_records<T, MAXA>(P, S, root, qs, L, ro, rz);
+        T a = 0, b = 0, c = 0, e = 0, f = 0, ii = 0;  // symmetric J J^T entries
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) {
+            T J[3];
+            jcol<T, 3>(S[s], ro[s], rz[s], L, J);
+            a += J[0] * J[0]; b += J[0] * J[1]; c += J[0] * J[2];
+            e += J[1] * J[1]; f += J[1] * J[2]; ii += J[2] * J[2];
+        }
+        // `jac * transpose(jac) .+ sr_weight`: +1.0 on EVERY entry (reference quirk)
+        a += T(1); b += T(1); c += T(1); e += T(1); f += T(1); ii += T(1);
+        const T d = b, g = c, h = f;  // symmetric
+        const T A_ = e * ii - f * h, B_ = -(d * ii - f * g), C_ = d * h - e * g;
+        const T det = a * A_ + b * B_ + c * C_;
+        const T i00 = A_ / det, i01 = -(b * ii - c * h) / det, i02 = (b * f - c * e) / det;
+        const T i10 = B_ / det, i11 = (a * ii - c * g) / det, i12 = -(a * f - c * d) / det;
+        const T i20 = C_ / det, i21 = -(a * h - b * g) / det, i22 = (a * e - b * d) / det;
+        const T dp0 = pd0 - L.t[0], dp1 = pd1 - L.t[1], dp2 = pd2 - L.t[2];
+        const T y0 = i00 * dp0 + i01 * dp1 + i02 * dp2;
+        const T y1 = i10 * dp0 + i11 * dp1 + i12 * dp2;
+        const T y2 = i20 * dp0 + i21 * dp1 + i22 * dp2;
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) {
+            T J[3];
+            jcol<T, 3>(S[s], ro[s], rz[s], L, J);
+            qs[s] += J[0] * y0 + J[1] * y1 + J[2] * y2;
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        if (c >= 0) q[(int64_t)c * ldq + i] = qs[s];
+    }
+}
+
+inline unsigned grid_of(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// phase-A sizes compiled (the stager pads the chain to one of these: pick_chain_bound)
+#define KIN_MAXA_DISPATCH(M, CALL) \
+    switch (M) {                   \
+    case 4: CALL(4); break;        \
+    case 8: CALL(8); break;        \
+    case 12: CALL(12); break;      \
+    case 16: CALL(16); break;      \
+    default: CALL(32); break;      \
+    }
+
+template <typename T>
+hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid(grid_of(n, g.block)), block(g.block);
+#define KIN_FK_LAUNCH(MA) \
+    hipLaunchKernelGGL((k_fk<T, MA>), grid, block, g.lds, st, P, steps, q, ldq, n, poses, ldp, jac, ldj)
+    KIN_MAXA_DISPATCH(g.maxA, KIN_FK_LAUNCH)
+#undef KIN_FK_LAUNCH
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
+                         const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
+                         int64_t lde, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step)};
+    const dim3 grid(grid_of(n, 256)), block(256);
+#define KIN_IK6(MA) \
+    hipLaunchKernelGGL((k_ik_dls<T, MA, 6>), grid, block, 0, st, P, steps, at, target, ldt, q, ldq, n, iters, err, lde)
+#define KIN_IK3(MA) \
+    hipLaunchKernelGGL((k_ik_dls<T, MA, 3>), grid, block, 0, st, P, steps, at, target, ldt, q, ldq, n, iters, err, lde)
+    if (a.with_rot) {
+        KIN_MAXA_DISPATCH(g.maxA, KIN_IK6)
+    } else {
+        KIN_MAXA_DISPATCH(g.maxA, KIN_IK3)
+    }
+#undef KIN_IK6
+#undef KIN_IK3
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
+                           int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid(grid_of(n, 256)), block(256);
+#define KIN_NK_LAUNCH(MA) hipLaunchKernelGGL((k_nakamura<T, MA>), grid, block, 0, st, P, steps, pts, ldpt, q, ldq, n)
+    KIN_MAXA_DISPATCH(g.maxA, KIN_NK_LAUNCH)
+#undef KIN_NK_LAUNCH
+    return hipGetLastError();
+}
+
+#define KIN_INSTANTIATE(T)                                                                                    \
+    template hipError_t launch_fk<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, \
+                                     int64_t, T*, int64_t, T*, int64_t, hipStream_t);                        \
+    template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, \
+                                         const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,     \
+                                         hipStream_t);                                                        \
+    template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
+                                           int64_t, T*, int64_t, int64_t, hipStream_t);
+KIN_INSTANTIATE(float)
+KIN_INSTANTIATE(double)
+
+}  // namespace kinhip

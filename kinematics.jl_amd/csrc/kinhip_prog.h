@@ -1,0 +1,68 @@
+// kinhip_prog.h -- staged evaluation program shared by the host stager
+// (kinhip_host.cpp) and the gfx950 kernels (kinhip_kernels.hip).
+//
+// A plan compiles the reference's per-link transform chain
+// (src/algorithm.jl:6-37 + joint_transform, src/mechanism.jl:90-103) into a
+// short list of steps.  Every step is
+//
+//     C <- C_src * F                     (3x4 rigid product, F staged on host)
+//     [record o = C.t, z = scale * C.col2]   (pre-motion world joint axis,
+//                                              src/algorithm.jl:42-54)
+//     C <- C * Rz(theta(q))  or  C <- C * Tz(scale * q)       (joint motion)
+//     [output  L = C * X]  [save C to an LDS slot]
+//
+// "Canonical" frames: the host folds a rotation A (A e_z = joint axis) into F
+// so that every moving joint turns about / slides along local z; X = A^T (and,
+// for joints held at a constant angle, their motion) restores the link frame
+// L of the reference.  Static chains (fixed joints and joints not driven by a
+// batch column, at m.angles) are pre-multiplied on the host in fp64 exactly
+// like joint_transform does it (quaternion path, `angle == 0.0` shortcut).
+#pragma once
+#include <stdint.h>
+
+namespace kinhip {
+
+enum : int32_t { MOT_NONE = 0, MOT_REV = 1, MOT_PRISM = 2 };
+enum : int32_t { SF_REC = 1, SF_HAS_X = 2, SF_SCALE = 4 };
+enum : int32_t { LOAD_NONE = -1, LOAD_ROOT = -2 };
+enum : int32_t { PF_JAC = 1, PF_WITH_ROT = 2, PF_RPY = 4, PF_ZERO = 8, PF_BASE = 16 };
+
+constexpr int kMaxChain = 32;  // phase-A steps (root -> spine link), register resident
+constexpr int kMaxJacCols = 64;
+constexpr int kMaxSlots = 8;
+
+template <typename T>
+struct KStep {
+    T F[12];   // row-major 3x4 [R | t]
+    T X[12];   // output correction (row-major 3x4), valid with SF_HAS_X
+    T scale;   // |axis| (revolute: angle map, prismatic: slide scale, record: z scale)
+    T lo, hi;  // joint limits of the driving column (IK clamps)
+    T pad0;
+    int32_t kind;   // MOT_* applied in the kernel
+    int32_t jkind;  // joint type for the Jacobian column (MOT_REV / MOT_PRISM)
+    int32_t qcol;   // batch column driving the motion (-1: none)
+    int32_t flags;  // SF_*
+    int32_t out;    // output index (-1: none)
+    int32_t load;   // LOAD_NONE: continue, LOAD_ROOT: root frame, >=0: LDS slot
+    int32_t save;   // LDS slot to save C into (-1: none)
+    int32_t pad1;
+    uint64_t colmask;  // Jacobian columns this record feeds (phase A only)
+};
+
+template <typename T>
+struct KProg {
+    int32_t nA;        // phase-A steps (root -> spine link, padded to the kernel's MAXA)
+    int32_t nS;        // total steps
+    int32_t n_slots;
+    int32_t rows;      // Jacobian rows (3 or 6)
+    int32_t n_jac;     // Jacobian columns before the base columns
+    int32_t flags;     // PF_*
+    int32_t base_col;  // q column of base x (PF_BASE)
+    int32_t last_has_x;
+    int32_t spine_out;  // output index of the spine link written after phase A (-1: none)
+    int32_t pad;
+    uint64_t zmask;    // irrelevant Jacobian columns (zero-filled with PF_ZERO)
+    T Xlast[12];       // spine link frame = C(after phase A) * Xlast
+};
+
+}  // namespace kinhip

@@ -1,0 +1,20 @@
+"""kinhip -- MI355X-native batched kinematics (FK, Jacobian, IK) for Kinematics.jl users.
+
+Python host mirror of the reference's API over the C-ABI library
+``libkinhip.so`` (include/kinhip.h).  The compute path is the gfx950 HIP
+engine only; importing this package on a machine without the built library
+fails loudly.
+"""
+from ._lib import KinError, LIB_PATH, lib  # noqa: F401
+from .mechanism import (  # noqa: F401
+    BoxMetaData, Joint, Link, Mechanism, Plan, SphereMetaData, add_new_link, child_joints, child_link,
+    child_links, find_joint, find_link, get_jacobian, get_jacobian_, get_jacobian_batch, get_joint_angles,
+    get_transform, get_transform_batch, inverse_kinematics_, is_relevant, isleaf, isroot, parent_joint,
+    parent_link, parse_urdf, point_inverse_kinematics_nakamura, rpy, set_joint_angles,
+)
+from .synth import uniform_configs  # noqa: F401
+
+FETCH_ARM_JOINTS = [
+    "torso_lift_joint", "shoulder_pan_joint", "shoulder_lift_joint", "upperarm_roll_joint",
+    "elbow_flex_joint", "forearm_roll_joint", "wrist_flex_joint", "wrist_roll_joint",
+]

@@ -1,0 +1,505 @@
+"""Host-side mirror of Kinematics.jl's Mechanism API over libkinhip.so.
+
+Mirrors the reference's exported names and their meaning (src/Kinematics.jl:45-73):
+``parse_urdf``, ``Mechanism``, ``Link``, ``Joint``, ``find_link`` /
+``find_joint`` (KeyError on unknown names), ``parent_link`` ...,
+``set_joint_angles`` / ``get_joint_angles``, ``is_relevant``,
+``add_new_link``, ``get_transform``, ``get_jacobian`` / ``get_jacobian_``
+(Julia's ``get_jacobian!``), ``rpy``.  The single-configuration calls run the
+HIP engine with a batch of one; the batched calls (``Plan``,
+``get_transform_batch``, ``get_jacobian_batch``) are the hot path.
+
+Array layout of the batched calls = Julia column-major ``Matrix{T}(N, k)``:
+torch tensors of shape ``(k, N)`` (configuration index fastest); poses
+``(n_links, 12, N)`` (3x4 column-major per link); Jacobians
+``(n_cols, rows, N)``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as K
+
+_DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
+
+
+# ---------------------------------------------------------------------------
+# data types (src/mechanism.jl:1-88)
+# ---------------------------------------------------------------------------
+@dataclass
+class BoxMetaData:
+    extents: np.ndarray
+    origin: np.ndarray  # 4x4
+
+
+@dataclass
+class SphereMetaData:
+    radius: float
+    origin: np.ndarray
+
+
+@dataclass(eq=False)
+class Link:
+    name: str
+    id: int = -1
+    pjoint_id: int = -1
+    cjoint_ids: list = field(default_factory=list)
+    plink_id: int = -1
+    clink_ids: list = field(default_factory=list)
+    geometric_meta_data: object = None
+    link_type: str = "URDF"
+    data: dict = field(default_factory=dict)
+
+
+@dataclass(eq=False)
+class Joint:
+    name: str
+    id: int
+    plink_id: int
+    clink_id: int
+    pose: np.ndarray  # 4x4
+    jtype: str        # "revolute" (incl. continuous), "prismatic", "fixed"
+    axis: np.ndarray
+    lower_limit: float = -math.inf
+    upper_limit: float = math.inf
+
+
+_JT = {K.KIN_JOINT_FIXED: "fixed", K.KIN_JOINT_REVOLUTE: "revolute", K.KIN_JOINT_PRISMATIC: "prismatic"}
+_JT_INV = {v: k for k, v in _JT.items()}
+
+
+def _i32(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.int32))
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _ids(items) -> np.ndarray:
+    return _i32([it.id if hasattr(it, "id") else int(it) for it in items])
+
+
+class Mechanism:
+    """Kinematic tree + state (src/mechanism.jl:147-181), backed by a kin_model."""
+
+    def __init__(self, links: list, joints: list, with_base: bool = False, name: str = "basic"):
+        self.name = name
+        self.links = links
+        self.joints = joints
+        self.with_base = bool(with_base)
+        self.linkid_map = {l.name: l.id for l in links}
+        self.jointid_map = {j.name: j.id for j in joints}
+        self.angles = np.zeros(len(joints))
+        self.base_pose = np.zeros(3)
+        self._angles_synced = True
+        self._model = C.c_void_p()
+        self._create_model()
+
+    # -- native model ---------------------------------------------------------
+    def _tree_arrays(self):
+        J = len(self.joints)
+        return [_i32([_JT_INV[j.jtype] for j in self.joints]), _i32([j.plink_id for j in self.joints]),
+                _i32([j.clink_id for j in self.joints]),
+                np.ascontiguousarray(np.array([np.asarray(j.pose, np.float64).T.reshape(16) for j in self.joints]
+                                              ).reshape(J * 16) if J else np.zeros(16)),
+                np.ascontiguousarray(np.array([j.axis for j in self.joints], np.float64).reshape(-1) if J else np.zeros(3)),
+                np.array([j.lower_limit for j in self.joints], np.float64),
+                np.array([j.upper_limit for j in self.joints], np.float64)]
+
+    def _create_model(self):
+        arrs = self._tree_arrays()
+        d = K.TreeDesc(len(self.links), len(self.joints), *[_p(a).value for a in arrs], int(self.with_base))
+        K.check(K.lib().kin_model_create(C.byref(d), C.byref(self._model)))
+
+    def __del__(self):
+        if getattr(self, "_model", None) and K._lib is not None:
+            K._lib.kin_model_destroy(self._model)
+            self._model = None
+
+    def _sync_angles(self):
+        if not self._angles_synced:
+            a = np.ascontiguousarray(self.angles, np.float64)
+            K.check(K.lib().kin_model_set_angles(self._model, _p(a)))
+            self._angles_synced = True
+
+    # -- tree queries (src/mechanism.jl:183-197) -----------------------------
+    def find_link(self, name) -> Link:
+        return self.links[self.linkid_map[name] - 1]  # KeyError like Julia's Dict
+
+    def find_joint(self, name) -> Joint:
+        return self.joints[self.jointid_map[name] - 1]
+
+    def parent_link(self, x):
+        return self.links[x.plink_id - 1]
+
+    def child_link(self, joint: Joint) -> Link:
+        return self.links[joint.clink_id - 1]
+
+    def child_links(self, link: Link):
+        return [self.links[i - 1] for i in link.clink_ids]
+
+    def parent_joint(self, link: Link) -> Joint:
+        return self.joints[link.pjoint_id - 1]
+
+    def child_joints(self, link: Link):
+        return [self.joints[i - 1] for i in link.cjoint_ids]
+
+    def is_relevant(self, joint: Joint, link: Link) -> bool:
+        out = C.c_int32()
+        K.check(K.lib().kin_model_is_relevant(self._model, joint.id, link.id, C.byref(out)))
+        return bool(out.value)
+
+    # -- state (src/mechanism.jl:197-231) ------------------------------------
+    def joint_angle(self, joint: Joint) -> float:
+        return float(self.angles[joint.id - 1])
+
+    def set_joint_angle(self, joint: Joint, angle: float):
+        self.angles[joint.id - 1] = angle
+        self._angles_synced = False
+
+    def set_base_pose(self, vec):
+        self.base_pose = np.asarray(vec, np.float64).copy()
+
+    def set_joint_angles(self, joints: Sequence[Joint], angles):
+        angles = np.asarray(angles, np.float64)
+        n = len(joints)
+        assert angles.size == n + (3 if self.with_base else 0)
+        for j, a in zip(joints, angles[:n]):
+            self.angles[j.id - 1] = a
+        if self.with_base:
+            self.base_pose = angles[n:n + 3].copy()
+        self._angles_synced = False
+
+    def get_joint_angles(self, joints: Sequence[Joint]) -> np.ndarray:
+        out = [self.angles[j.id - 1] for j in joints]
+        if self.with_base:
+            out += list(self.base_pose)
+        return np.array(out, np.float64)
+
+    # -- add_new_link (src/mechanism.jl:233-267) ------------------------------
+    def add_new_link(self, new_link: Link, parent: Link, pose_or_position):
+        T = np.asarray(pose_or_position, np.float64)
+        if T.shape == (3,):
+            P = np.eye(4)
+            P[:3, 3] = T
+            T = P
+        T16 = np.ascontiguousarray(T.T.reshape(16))
+        nid = C.c_int32()
+        K.check(K.lib().kin_model_add_link(self._model, parent.id, _p(T16), C.byref(nid)))
+        hid = len(self.links) + 1
+        assert nid.value == hid
+        jid = len(self.joints) + 1
+        parent.clink_ids.append(hid)
+        parent.cjoint_ids.append(jid)
+        jnt = Joint(new_link.name + "_joint", jid, parent.id, hid, T.copy(), "fixed", np.array([1.0, 0, 0]))
+        new_link.id, new_link.pjoint_id, new_link.plink_id = hid, jid, parent.id
+        new_link.cjoint_ids, new_link.clink_ids, new_link.data = [], [], {}
+        self.links.append(new_link)
+        self.joints.append(jnt)
+        self.linkid_map[new_link.name] = hid
+        self.jointid_map[jnt.name] = jid
+        self.angles = np.append(self.angles, 0.0)
+        self._angles_synced = False
+        return new_link
+
+    # -- batched hot path -------------------------------------------------------
+    def plan(self, q_joints: Sequence[Joint], out_links: Sequence[Link] = (), jac_link: Optional[Link] = None,
+             jac_joints: Optional[Sequence[Joint]] = None, with_rot: bool = True, rpy_jac: bool = False,
+             zero_fill: bool = True, dtype=torch.float32) -> "Plan":
+        self._sync_angles()
+        return Plan(self, q_joints, out_links, jac_link, jac_joints, with_rot, rpy_jac, zero_fill, dtype)
+
+
+class Plan:
+    """A staged, device-resident evaluation program (kin_plan)."""
+
+    def __init__(self, m: Mechanism, q_joints, out_links, jac_link, jac_joints, with_rot, rpy_jac, zero_fill,
+                 dtype):
+        if dtype not in _DT:
+            raise TypeError("dtype must be torch.float32 or torch.float64")
+        self.m, self.dtype = m, dtype
+        self._q = _ids(q_joints)
+        self._o = _ids(out_links)
+        self._jl = 0 if jac_link is None else jac_link.id
+        if jac_link is not None and jac_joints is None:
+            jac_joints = q_joints
+        self._j = _ids(jac_joints or [])
+        flags = (K.KIN_WITH_ROT if with_rot else 0) | (K.KIN_RPY_JAC if rpy_jac else 0) | \
+                (K.KIN_ZERO_FILL if zero_fill else 0)
+        self.zero_fill = zero_fill
+        d = K.PlanDesc(_DT[dtype], self._q.size, _p(self._q).value, self._o.size, _p(self._o).value,
+                       self._jl, self._j.size, _p(self._j).value, flags)
+        self._h = C.c_void_p()
+        rc = K.lib().kin_plan_create(m._model, C.byref(d), C.byref(self._h))
+        if rc != K.KIN_OK:
+            msg = K.lib().kin_last_error().decode()
+            raise K.error_class(rc)(msg) if rc in (K.KIN_E_KEY, K.KIN_E_METHOD) else K.KinError(rc, msg)
+        nq, rows, cols = C.c_int32(), C.c_int32(), C.c_int32()
+        K.check(K.lib().kin_plan_shape(self._h, C.byref(nq), C.byref(rows), C.byref(cols)))
+        self.n_qcols, self.jac_rows, self.jac_cols = nq.value, rows.value, cols.value
+        self.n_out = self._o.size
+
+    def __del__(self):
+        if getattr(self, "_h", None) and K._lib is not None:
+            K._lib.kin_plan_destroy(self._h)
+            self._h = None
+
+    def _check_q(self, Q: torch.Tensor) -> int:
+        if not Q.is_cuda or Q.dtype != self.dtype or Q.dim() != 2 or Q.shape[0] != self.n_qcols:
+            raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_qcols}, N)")
+        if Q.stride(1) != 1:
+            raise ValueError("Q must be configuration-contiguous (stride(1) == 1)")
+        return Q.shape[1]
+
+    def run(self, Q: torch.Tensor, poses: Optional[torch.Tensor] = None, jac: Optional[torch.Tensor] = None,
+            stream: Optional[torch.cuda.Stream] = None):
+        """Evaluate N configurations; returns (poses [n_out,12,N], jac [cols,rows,N] or None). Async."""
+        N = self._check_q(Q)
+        dev = Q.device
+        if poses is None and self.n_out:
+            poses = torch.empty((self.n_out, 12, N), dtype=self.dtype, device=dev)
+        if jac is None and self._jl:
+            alloc = torch.zeros if not self.zero_fill else torch.empty
+            jac = alloc((self.jac_cols, self.jac_rows, N), dtype=self.dtype, device=dev)
+        for t, shape in ((poses, (self.n_out, 12, N)), (jac, (self.jac_cols, self.jac_rows, N))):
+            if t is not None and (tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != self.dtype):
+                raise ValueError(f"output must be a contiguous {self.dtype} tensor of shape {shape}")
+        st = (stream or torch.cuda.current_stream(dev)).cuda_stream
+        ldq = Q.stride(0) if self.n_qcols else N
+        K.check(K.lib().kin_plan_run(self._h, Q.data_ptr() if self.n_qcols else None, ldq, N,
+                                     poses.data_ptr() if poses is not None else None, N,
+                                     jac.data_ptr() if jac is not None else None, N, st))
+        return poses, jac
+
+    def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
+               max_step=0.5, with_rot=True, stream=None):
+        """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N])."""
+        N = self._check_q(Q)
+        if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
+            raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
+        iters = torch.empty(N, dtype=torch.int32, device=Q.device)
+        err = torch.empty((2, N), dtype=self.dtype, device=Q.device)
+        prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot))
+        st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+        K.check(K.lib().kin_ik_dls_batch(self._h, C.byref(prm), targets.data_ptr(), N, Q.data_ptr(), Q.stride(0), N,
+                                         iters.data_ptr(), err.data_ptr(), N, st))
+        return Q, iters, err
+
+    def point_ik_nakamura(self, points: torch.Tensor, Q: torch.Tensor, stream=None):
+        N = self._check_q(Q)
+        if points.shape != (3, N) or points.dtype != self.dtype or not points.is_contiguous():
+            raise ValueError("points must be a contiguous (3, N) tensor of the plan dtype")
+        st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+        K.check(K.lib().kin_point_ik_nakamura_batch(self._h, points.data_ptr(), N, Q.data_ptr(), Q.stride(0), N, st))
+        return Q
+
+
+# ---------------------------------------------------------------------------
+# URDF (src/load_urdf.jl:20-80) through the native parser
+# ---------------------------------------------------------------------------
+def parse_urdf(urdf_path: str, with_base: bool = False, name: Optional[str] = None) -> Mechanism:
+    L = K.lib()
+    u = C.c_void_p()
+    K.check(L.kin_urdf_parse_file(urdf_path.encode(), C.byref(u)))
+    try:
+        d = K.TreeDesc()
+        K.check(L.kin_urdf_tree(u, int(with_base), C.byref(d)))
+        nl, nj = d.n_links, d.n_joints
+        as_np = lambda ptr, n, ct: np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy() if n else \
+            np.zeros(0)
+        jt = as_np(d.joint_type, nj, C.c_int32)
+        jp = as_np(d.joint_plink, nj, C.c_int32)
+        jc = as_np(d.joint_clink, nj, C.c_int32)
+        pose = as_np(d.joint_pose, 16 * nj, C.c_double).reshape(nj, 16)
+        axis = as_np(d.joint_axis, 3 * nj, C.c_double).reshape(nj, 3)
+        lo = as_np(d.joint_lower, nj, C.c_double)
+        hi = as_np(d.joint_upper, nj, C.c_double)
+        nm = C.c_char_p()
+        links = []
+        for i in range(1, nl + 1):
+            K.check(L.kin_urdf_link_name(u, i, C.byref(nm)))
+            has = C.c_int32()
+            ext = np.zeros(3)
+            org = np.zeros(16)
+            K.check(L.kin_urdf_link_box(u, i, C.byref(has), _p(ext), _p(org)))
+            meta = BoxMetaData(ext, org.reshape(4, 4).T.copy()) if has.value else None
+            links.append(Link(nm.value.decode(), i, geometric_meta_data=meta))
+        joints = []
+        for j in range(nj):
+            K.check(L.kin_urdf_joint_name(u, j + 1, C.byref(nm)))
+            joints.append(Joint(nm.value.decode(), j + 1, int(jp[j]), int(jc[j]), pose[j].reshape(4, 4).T.copy(),
+                                _JT[int(jt[j])], axis[j].copy(), float(lo[j]), float(hi[j])))
+            p, c = links[jp[j] - 1], links[jc[j] - 1]
+            p.cjoint_ids.append(j + 1)
+            p.clink_ids.append(int(jc[j]))
+            c.pjoint_id, c.plink_id = j + 1, int(jp[j])
+    finally:
+        L.kin_urdf_destroy(u)
+    return Mechanism(links, joints, with_base=with_base, name=name or "basic")
+
+
+# ---------------------------------------------------------------------------
+# Julia-style free functions (src/Kinematics.jl exports)
+# ---------------------------------------------------------------------------
+def find_link(m: Mechanism, name):
+    return m.find_link(name)
+
+
+def find_joint(m: Mechanism, name):
+    return m.find_joint(name)
+
+
+def parent_link(m, x):
+    return m.parent_link(x)
+
+
+def child_link(m, joint):
+    return m.child_link(joint)
+
+
+def child_links(m, link):
+    return m.child_links(link)
+
+
+def parent_joint(m, link):
+    return m.parent_joint(link)
+
+
+def child_joints(m, link):
+    return m.child_joints(link)
+
+
+def isroot(link: Link) -> bool:
+    return link.plink_id == -1
+
+
+def isleaf(link: Link) -> bool:
+    return len(link.clink_ids) == 0
+
+
+def is_relevant(m: Mechanism, joint: Joint, link: Link) -> bool:
+    return m.is_relevant(joint, link)
+
+
+def set_joint_angles(m: Mechanism, joints, angles):
+    m.set_joint_angles(joints, angles)
+
+
+def get_joint_angles(m: Mechanism, joints):
+    return m.get_joint_angles(joints)
+
+
+def add_new_link(m: Mechanism, new_link: Link, parent: Link, pose_or_position):
+    return m.add_new_link(new_link, parent, pose_or_position)
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("kinhip: no HIP device visible (the engine has no CPU path)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _single_q(m: Mechanism, dev):
+    q = list(m.angles) + (list(m.base_pose) if m.with_base else [])
+    return torch.tensor(q, dtype=torch.float64, device=dev).reshape(-1, 1)
+
+
+def get_transform(m: Mechanism, link: Link) -> np.ndarray:
+    """World pose (4x4) of ``link`` at the mechanism's current angles (src/algorithm.jl:1-4)."""
+    dev = _device()
+    key = ("tf", link.id, len(m.joints))
+    plan = m.__dict__.setdefault("_single_plans", {}).get(key)
+    if plan is None:
+        plan = m.plan(m.joints, out_links=[link], dtype=torch.float64)
+        m._single_plans[key] = plan
+    poses, _ = plan.run(_single_q(m, dev))
+    T = np.eye(4)
+    T[:3, :4] = poses[0, :, 0].cpu().numpy().reshape(4, 3).T
+    return T
+
+
+def get_jacobian_(m: Mechanism, link: Link, joints, with_rot: bool, mat_out: np.ndarray, rpy_jac=False):
+    """``get_jacobian!`` (src/algorithm.jl:83-106): writes relevant columns into mat_out."""
+    dev = _device()
+    key = ("jac", link.id, tuple(j.id for j in joints), bool(with_rot), bool(rpy_jac), len(m.joints))
+    plans = m.__dict__.setdefault("_single_plans", {})
+    plan = plans.get(key)
+    ids = list(range(1, len(m.joints) + 1))
+    if plan is None:
+        plan = Plan(m, ids, [], link, joints, with_rot, rpy_jac, False, torch.float64)
+        plans[key] = plan
+    jac = torch.as_tensor(np.ascontiguousarray(np.asarray(mat_out, np.float64).T)).to(dev).reshape(
+        plan.jac_cols, plan.jac_rows, 1).contiguous()
+    # the plan's Jacobian columns are `joints` (+ base); its q columns are every joint
+    plan.run(_single_q(m, dev), jac=jac)
+    mat_out[...] = jac[:, :, 0].cpu().numpy().T
+    return mat_out
+
+
+def get_jacobian(m: Mechanism, link: Link, joints, with_rot: bool, rpy_jac=False) -> np.ndarray:
+    rows = 6 if with_rot else 3
+    cols = len(joints) + (3 if m.with_base else 0)
+    J = np.zeros((rows, cols))
+    return get_jacobian_(m, link, joints, with_rot, J, rpy_jac=rpy_jac)
+
+
+def get_transform_batch(m: Mechanism, links, joints, Q: torch.Tensor):
+    """Batched get_transform: Q (len(joints)[+3], N) -> poses (len(links), 12, N)."""
+    plan = m.plan(joints, out_links=links, dtype=Q.dtype)
+    return plan.run(Q)[0]
+
+
+def get_jacobian_batch(m: Mechanism, link, joints, Q: torch.Tensor, with_rot=True, rpy_jac=False):
+    """Batched get_transform + get_jacobian: -> (pose (12, N), jac (cols, rows, N))."""
+    plan = m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=with_rot, rpy_jac=rpy_jac,
+                  dtype=Q.dtype)
+    poses, jac = plan.run(Q)
+    return poses[0], jac
+
+
+def rpy(T) -> np.ndarray:
+    """RotZYX angles [roll, pitch, yaw] of a 4x4 (src/transform.jl:45-48)."""
+    R = np.asarray(T)[:3, :3]
+    t1 = math.atan2(R[1, 0], R[0, 0])
+    c1, s1 = math.cos(t1), math.sin(t1)
+    t2 = math.atan2(-R[2, 0], R[1, 0] * s1 + R[0, 0] * c1)
+    t3 = math.atan2(R[0, 2] * s1 - R[1, 2] * c1, R[1, 1] * c1 - R[0, 1] * s1)
+    return np.array([t3, t2, t1])
+
+
+def point_inverse_kinematics_nakamura(m: Mechanism, link: Link, joints, point_desired) -> np.ndarray:
+    """src/algorithm.jl:116-131 on the GPU (batch of one); returns the angles."""
+    dev = _device()
+    plan = m.plan(joints, jac_link=link, jac_joints=joints, with_rot=False, dtype=torch.float64)
+    Q = torch.tensor([m.angles[j.id - 1] for j in joints], dtype=torch.float64, device=dev).reshape(-1, 1)
+    pts = torch.tensor(np.asarray(point_desired, np.float64), device=dev).reshape(3, 1).contiguous()
+    plan.point_ik_nakamura(pts, Q)
+    return Q[:, 0].cpu().numpy()
+
+
+def inverse_kinematics_(m: Mechanism, link: Link, joints, target_pose, ftol=1e-5, with_rot=True, max_iters=64,
+                        lam=1e-2, max_step=0.5):
+    """``inverse_kinematics!`` (src/inverse_kinematics.jl:23-30) via the batched DLS kernel.
+
+    Returns (q, status) with status ``:FTOL_REACHED`` when converged (position
+    and rotation error below 1e-3, the reference test's acceptance) else
+    ``:MAXEVAL_REACHED``.  Sets the mechanism's angles to the solution.
+    """
+    dev = _device()
+    plan = m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=True, dtype=torch.float64)
+    Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    T = np.asarray(target_pose, np.float64)
+    tgt = torch.tensor(T[:3, :4].T.reshape(12), device=dev).reshape(12, 1).contiguous()
+    Q, iters, err = plan.ik_dls(tgt, Q, max_iters=max_iters, lam=lam, tol_pos=1e-3 * 0.1, tol_rot=1e-3 * 0.1,
+                                max_step=max_step, with_rot=with_rot)
+    q = Q[:, 0].cpu().numpy()
+    m.set_joint_angles(joints, q)
+    ok = int(iters[0].item()) < max_iters
+    return q, (":FTOL_REACHED" if ok else ":MAXEVAL_REACHED")

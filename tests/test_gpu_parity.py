@@ -1,0 +1,328 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the CPU oracle and the golden fixtures.
+
+Tolerances (stated per BASELINE north star: poses / Jacobian entries within 1e-6 absolute):
+  fp64 kernels: 1e-9 absolute vs the oracle (observed ~1e-15)
+  fp32 kernels: 2e-5 absolute vs the oracle evaluated at the fp32-rounded angles
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import ARM, EXAMPLE_LINKS, golden
+
+import kinhip
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float64: 1e-9, torch.float32: 2e-5}
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def fetch_tree():
+    return O.parse_urdf_tree(golden("fetch.urdf"))
+
+
+def _fetch(with_base=False):
+    m = kinhip.parse_urdf(golden("fetch.urdf"), with_base=with_base)
+    return m, [m.find_joint(n) for n in ARM]
+
+
+def _rand_q(n, ncol, seed, dtype, dev, lo=-2.5, hi=2.5):
+    g = torch.Generator().manual_seed(seed)
+    q = torch.rand((ncol, n), generator=g, dtype=torch.float64) * (hi - lo) + lo
+    return q.to(dtype).to(dev)
+
+
+# ---------------------------------------------------------------- fixtures ---
+@pytest.mark.parametrize("with_base", [False, True])
+def test_ground_truth_json_on_gpu(dev, with_base):
+    """test/test_kinematics.jl:10-41 through the GPU (PR2 fragment, fp64), all 9 links, twice."""
+    gt = json.load(open(golden("ground_truth.json")))
+    m = kinhip.parse_urdf(golden("pr2_torso_rarm.urdf"), with_base=with_base)
+    joints = [m.find_joint(n) for n in gt["joint_names"]]
+    links = [m.find_link(n) for n in gt["link_names"]]
+    angles = list(gt["angle_vector"]) + ([0.3, 0.3, 0.3] if with_base else [])
+    Q = torch.tensor(angles, dtype=torch.float64, device=dev).reshape(-1, 1).repeat(1, 3).contiguous()
+    poses = kinhip.get_transform_batch(m, links, joints, Q).cpu().numpy()
+    th = 0.3
+    Rz = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
+    for rep in range(2):
+        for k, pg in enumerate(gt["pose_list"]):
+            T = np.eye(4)
+            T[:3, :4] = poses[k, :, rep].reshape(4, 3).T
+            r = kinhip.rpy(T)
+            ypr = np.array([r[2], r[1], r[0]])
+            pg = np.asarray(pg)
+            if with_base:
+                np.testing.assert_allclose(T[:3, 3], Rz @ pg[:3] + [0.3, 0.3, 0], atol=1e-6)
+                np.testing.assert_allclose(ypr, pg[3:] + [0.3, 0, 0], atol=1e-6)
+            else:
+                np.testing.assert_allclose(T[:3, 3], pg[:3], atol=1e-6)
+                np.testing.assert_allclose(ypr, pg[3:], atol=1e-6)
+    # and the single-configuration API (get_transform) on the same fixture
+    m.set_joint_angles(joints, angles)
+    T = kinhip.get_transform(m, links[5])
+    ref = np.asarray(gt["pose_list"][5])
+    if not with_base:
+        np.testing.assert_allclose(T[:3, 3], ref[:3], atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_golden_fetch_fixture(dev, dtype):
+    g = np.load(golden("fetch_fk_jac_golden.npz"))
+    m, arm = _fetch()
+    Q = torch.tensor(g["q"], dtype=dtype, device=dev).contiguous()
+    tol = 1e-9 if dtype == torch.float64 else 5e-5  # fp32: fixture angles are fp64 (not re-rounded)
+    poses = kinhip.get_transform_batch(m, m.links, arm, Q).double().cpu().numpy()
+    np.testing.assert_allclose(poses, g["poses"], atol=tol)
+    gl = m.find_link("gripper_link")
+    pose, jac = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True)
+    np.testing.assert_allclose(jac.double().cpu().numpy(), g["jac_geo"], atol=tol)
+    np.testing.assert_allclose(pose.double().cpu().numpy(), g["poses"][gl.id - 1], atol=tol)
+    _, jr = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True, rpy_jac=True)
+    jr = jr.double().cpu().numpy()
+    ok = np.abs(np.cos(np.arcsin(np.clip(-g["poses"][gl.id - 1][2], -1, 1)))) > 1e-2  # away from pitch = +-pi/2
+    np.testing.assert_allclose(jr[:, :, ok], g["jac_rpy"][:, :, ok], atol=tol * 10)
+    mb, armb = _fetch(with_base=True)
+    Qb = torch.tensor(g["qb"], dtype=dtype, device=dev).contiguous()
+    pb, jb = kinhip.get_jacobian_batch(mb, mb.find_link("gripper_link"), armb, Qb)
+    np.testing.assert_allclose(pb.double().cpu().numpy(), g["pose_base"], atol=tol)
+    np.testing.assert_allclose(jb.double().cpu().numpy(), g["jac_base"], atol=tol)
+
+
+# ------------------------------------------------------------ vs oracle ------
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("rpy_jac", [False, True])
+def test_fk_jac_vs_oracle(dev, fetch_tree, dtype, with_base, rpy_jac):
+    m, arm = _fetch(with_base)
+    N = 3000  # not a multiple of the block size
+    Q = _rand_q(N, 8 + (3 if with_base else 0), 7, dtype, dev)
+    gl = m.find_link("gripper_link")
+    pose, jac = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True, rpy_jac=rpy_jac)
+    om = O.OracleMech(fetch_tree, with_base=with_base)
+    qd = Q.double().cpu().numpy()
+    ps, js = om.fk_jac_batch(qd, [j.id for j in arm], gl.id, [j.id for j in arm], True, rpy_jac)
+    np.testing.assert_allclose(pose.double().cpu().numpy(), ps, atol=TOL[dtype])
+    jg = jac.double().cpu().numpy()
+    if rpy_jac:  # rpy rows blow up at pitch = +-pi/2; compare where cos(pitch) is not tiny
+        ok = np.sqrt(ps[0] ** 2 + ps[1] ** 2) > 0.05
+        np.testing.assert_allclose(jg[:, :, ok], js[:, :, ok], atol=TOL[dtype] * 20)
+    else:
+        np.testing.assert_allclose(jg, js, atol=TOL[dtype])
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_multi_link_fk_vs_oracle(dev, fetch_tree, dtype):
+    """Config 2 shape (exampel.jl:11 links) and every link, with LDS branch slots."""
+    m, arm = _fetch()
+    Q = _rand_q(2049, 8, 11, dtype, dev)
+    om = O.OracleMech(fetch_tree)
+    for names in (EXAMPLE_LINKS, [l.name for l in m.links], ["r_gripper_finger_link", "head_pan_link", "base_link",
+                                                                "laser_link", "l_gripper_finger_link"]):
+        links = [m.find_link(n) for n in names]
+        poses = kinhip.get_transform_batch(m, links, arm, Q).double().cpu().numpy()
+        ref = om.fk_batch(Q.double().cpu().numpy(), [j.id for j in arm], [l.id for l in links])
+        np.testing.assert_allclose(poses, ref, atol=TOL[dtype])
+
+
+def test_jacobian_column_semantics(dev, fetch_tree):
+    """get_jacobian! (untouched) vs get_jacobian (zeros), irrelevant and repeated columns,
+    q joints != Jacobian joints, non-batched joints at m.angles (src/algorithm.jl:83-114)."""
+    m, arm = _fetch()
+    head = m.find_joint("head_pan_joint")
+    jj = [arm[3], head, arm[0], arm[3], arm[6]]  # repeated column, irrelevant head column
+    gl = m.find_link("gripper_link")
+    qj = arm[:5]  # joints 6..8 stay at m.angles
+    defaults = np.zeros(len(m.joints))
+    for j, a in zip(arm[5:], [0.4, -0.7, 1.1]):
+        defaults[j.id - 1] = a
+    m.angles[:] = defaults
+    m._angles_synced = False
+    N = 700
+    Q = _rand_q(N, 5, 3, torch.float64, dev)
+    om = O.OracleMech(fetch_tree)
+    om_ids = [j.id for j in qj] + [j.id for j in arm[5:]]
+    qfull = np.vstack([Q.cpu().numpy(), np.tile(np.array([[0.4], [-0.7], [1.1]]), (1, N))])
+    for zero in (True, False):
+        plan = m.plan(qj, out_links=[gl], jac_link=gl, jac_joints=jj, zero_fill=zero, dtype=torch.float64)
+        init = torch.full((len(jj), 6, N), 9.0, dtype=torch.float64, device=dev)
+        _, jac = plan.run(Q, jac=init)
+        init_np = np.full((len(jj), 6, N), 9.0)
+        _, ref = om.fk_jac_batch(qfull, om_ids, gl.id, [j.id for j in jj], True, False, zero_fill=zero,
+                                 jac_init=init_np)
+        np.testing.assert_allclose(jac.cpu().numpy(), ref, atol=1e-9)
+        if not zero:
+            assert np.all(jac.cpu().numpy()[1] == 9.0)       # head column untouched
+            assert np.all(jac.cpu().numpy()[2, 3:] == 9.0)   # prismatic torso: rows 4:6 untouched
+
+
+def test_fd_jacobian_on_gpu(dev):
+    """Analytic GPU Jacobian vs forward differences of GPU FK (test_kinematics.jl:57-66)."""
+    m, arm = _fetch(with_base=True)
+    gl = m.find_link("gripper_link")
+    N = 256
+    Q = _rand_q(N, 11, 5, torch.float64, dev, -1.5, 1.5)
+    pose, jac = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True)
+    eps = 1e-7
+    for c in range(11):
+        Q1 = Q.clone()
+        Q1[c] += eps
+        p1 = kinhip.get_transform_batch(m, [gl], arm, Q1)[0]
+        fd = (p1[9:12] - pose[9:12]) / eps
+        torch.testing.assert_close(fd, jac[c, :3], atol=1e-5, rtol=0)
+
+
+def test_edge_sizes_and_strides(dev, fetch_tree):
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
+    om = O.OracleMech(fetch_tree)
+    for N in (1, 63, 64, 65, 257):
+        Q = _rand_q(N, 8, N, torch.float64, dev)
+        poses, jac = plan.run(Q)
+        ps, js = om.fk_jac_batch(Q.cpu().numpy(), [j.id for j in arm], gl.id, [j.id for j in arm])
+        np.testing.assert_allclose(poses[0].cpu().numpy(), ps, atol=1e-9)
+        np.testing.assert_allclose(jac.cpu().numpy(), js, atol=1e-9)
+    # ldq > N: a column-padded Julia matrix view
+    big = _rand_q(300, 8, 1, torch.float64, dev)
+    Qv = big[:, :200]
+    poses, _ = plan.run(Qv)
+    ps, _ = om.fk_jac_batch(Qv.cpu().numpy(), [j.id for j in arm], gl.id, [j.id for j in arm])
+    np.testing.assert_allclose(poses[0].cpu().numpy(), ps, atol=1e-9)
+    # N = 0 is a no-op
+    plan.run(torch.empty((8, 0), dtype=torch.float64, device=dev))
+
+
+def test_large_batch_properties(dev, fetch_tree):
+    """BASELINE size (2^20, fp32): size-independent properties + a strided oracle sample."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    lo = [j.lower_limit for j in arm]
+    hi = [j.upper_limit for j in arm]
+    N = 1 << 20
+    Q = kinhip.uniform_configs(lo, hi, N, dtype=torch.float32, device=dev)
+    pose, jac = kinhip.get_jacobian_batch(m, gl, arm, Q)
+    R = pose[:9].reshape(3, 3, N).permute(2, 1, 0)  # [N, row, col]
+    eye = torch.eye(3, device=dev).expand(N, 3, 3)
+    assert float((R @ R.transpose(1, 2) - eye).abs().max()) < 5e-6
+    # angular rows of revolute columns are unit axes; torso (prismatic) linear rows too
+    nrm = jac[1:, 3:].norm(dim=1)
+    assert float((nrm - 1).abs().max()) < 1e-5
+    assert float((jac[0, :3].norm(dim=0) - 1).abs().max()) < 1e-5
+    # linear rows = z x (p - o) => orthogonal to z
+    dot = (jac[1:, :3] * jac[1:, 3:]).sum(1)
+    assert float(dot.abs().max()) < 1e-5
+    idx = torch.arange(0, N, 4099, device=dev)
+    om = O.OracleMech(fetch_tree)
+    ps, js = om.fk_jac_batch(Q[:, idx].double().cpu().numpy(), [j.id for j in arm], gl.id, [j.id for j in arm])
+    np.testing.assert_allclose(pose[:, idx].double().cpu().numpy(), ps, atol=2e-5)
+    np.testing.assert_allclose(jac[:, :, idx].double().cpu().numpy(), js, atol=2e-5)
+
+
+# -------------------------------------------------------------------- IK ------
+def test_nakamura_vs_oracle(dev, fetch_tree):
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    N = 512
+    plan = m.plan(arm, jac_link=gl, jac_joints=arm, with_rot=False, dtype=torch.float64)
+    Q0 = _rand_q(N, 8, 2, torch.float64, dev, -0.5, 0.5)
+    g = torch.Generator().manual_seed(3)
+    pts = (torch.rand((3, N), generator=g, dtype=torch.float64) * torch.tensor([[0.6], [1.0], [0.8]])
+           + torch.tensor([[0.3], [-0.5], [0.5]])).to(dev).contiguous()
+    Q = plan.point_ik_nakamura(pts, Q0.clone())
+    om = O.OracleMech(fetch_tree)
+    ref = om.point_ik_nakamura_batch(Q0.cpu().numpy(), [j.id for j in arm], gl.id, pts.cpu().numpy())
+    np.testing.assert_allclose(Q.cpu().numpy(), ref, atol=1e-7)
+    # single-config API
+    m.set_joint_angles(arm, np.zeros(8))
+    q1 = kinhip.point_inverse_kinematics_nakamura(m, gl, arm, [0.7, 0.2, 0.9])
+    r1 = O.OracleMech(fetch_tree).point_ik_nakamura(gl.id, [j.id for j in arm], [0.7, 0.2, 0.9])
+    np.testing.assert_allclose(q1, r1, atol=1e-8)
+
+
+def _targets(om, arm_ids, gl, N, seed, with_base=False):
+    lo = np.array([om.tree.joint_lower[i - 1] for i in arm_ids])
+    hi = np.array([om.tree.joint_upper[i - 1] for i in arm_ids])
+    lo = np.where(np.isfinite(lo), lo, -np.pi)
+    hi = np.where(np.isfinite(hi), hi, np.pi)
+    rng = np.random.default_rng(seed)
+    qt = lo[:, None] + (hi - lo)[:, None] * rng.random((len(arm_ids), N))
+    if with_base:
+        qt = np.vstack([qt, rng.uniform(-1, 1, (3, N))])
+    return om.fk_batch(qt, arm_ids, [gl])[0]
+
+
+def test_ik_dls_iterates_vs_oracle(dev, fetch_tree):
+    """fp64 kernel == fp64 oracle restatement of the same DLS (short runs, iterate parity)."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 512
+    tgt = _targets(om, ids, gl.id, N, 4)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
+    for iters in (1, 3, 8):
+        Q = torch.zeros((8, N), dtype=torch.float64, device=dev)
+        T = torch.tensor(tgt, device=dev).contiguous()
+        Q, it, err = plan.ik_dls(T, Q, max_iters=iters)
+        rq, rit, rerr = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, max_iters=iters)
+        np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+        np.testing.assert_array_equal(it.cpu().numpy(), rit)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ik_dls_acceptance(dev, fetch_tree, dtype):
+    """Reachable random targets: converged solutions meet the reference test's criteria
+    (|dp| <= 1e-3, |drpy| <= 1e-3, test/test_inverse_kinematics.jl:22-23), checked by the oracle's FK."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 4096
+    tgt = _targets(om, ids, gl.id, N, 9)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    Q = torch.zeros((8, N), dtype=dtype, device=dev)
+    Q, it, err = plan.ik_dls(torch.tensor(tgt, dtype=dtype, device=dev).contiguous(), Q, max_iters=64)
+    it = it.cpu().numpy()
+    conv = it < 64
+    assert conv.mean() > 0.5, conv.mean()
+    q = Q.double().cpu().numpy()
+    got = om.fk_batch(q, ids, [gl.id])[0]
+    dp = np.linalg.norm(got[9:] - tgt[9:], axis=0)
+    assert np.all(dp[conv] < 1e-3)
+    for k in np.nonzero(conv)[0][:200]:
+        Ta, Tt = np.eye(4), np.eye(4)
+        Ta[:3, :4] = got[:, k].reshape(4, 3).T
+        Tt[:3, :4] = tgt[:, k].reshape(4, 3).T
+        d = O.rpy(Ta) - O.rpy(Tt)
+        d = (d + np.pi) % (2 * np.pi) - np.pi
+        if abs(np.cos(O.rpy(Tt)[1])) > 1e-2:
+            assert np.all(np.abs(d) < 1e-3)
+    lo = np.array([j.lower_limit for j in arm])
+    hi = np.array([j.upper_limit for j in arm])
+    tol = 1e-6 if dtype == torch.float32 else 0
+    assert np.all(q >= lo[:, None] - tol) and np.all(q <= hi[:, None] + tol)
+
+
+def test_ik_reference_target(dev):
+    """test/test_inverse_kinematics.jl:1-25: Fetch gripper to (0.3, -0.4, 1.2), identity rotation."""
+    for with_base in (False, True):
+        m, arm = _fetch(with_base)
+        gl = m.find_link("gripper_link")
+        T = np.eye(4)
+        T[:3, 3] = [0.3, -0.4, 1.2]
+        q, status = kinhip.inverse_kinematics_(m, gl, arm, T, with_rot=True, max_iters=200)
+        assert status == ":FTOL_REACHED"
+        Tn = kinhip.get_transform(m, gl)
+        np.testing.assert_allclose(Tn[:3, 3], T[:3, 3], atol=1e-3)
+        np.testing.assert_allclose(kinhip.rpy(Tn), kinhip.rpy(T), atol=1e-3)

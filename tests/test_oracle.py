@@ -1,0 +1,196 @@
+"""CPU oracle pinned against the reference's own fixtures and tests (no GPU).
+
+Ports of the reference's test logic onto the C restatement:
+  test/test_kinematics.jl:1-41   FK vs data/ground_truth.json (PR2), with/without base, twice (cache)
+  test/test_kinematics.jl:43-73  analytic vs forward-difference Jacobian (eps 1e-7, atol 1e-5), rpy rows
+  test/test_mechanism.jl:1-68    tree / rptable facts (Fetch; PR2 facts through the fragment)
+  test/test_inverse_kinematics.jl:1-25  IK acceptance (|dp|, |drpy| <= 1e-3) -- DLS restatement
+plus an independent numpy formulation and the committed golden fixture.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import numpy_ref as R
+import oracle as O
+from conftest import ARM, golden
+
+
+@pytest.fixture(scope="module")
+def gt():
+    with open(golden("ground_truth.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def pr2():
+    return O.parse_urdf_tree(golden("pr2_torso_rarm.urdf"))
+
+
+@pytest.fixture(scope="module")
+def fetch():
+    return O.parse_urdf_tree(golden("fetch.urdf"))
+
+
+def _rotz(t):
+    return np.array([[np.cos(t), -np.sin(t), 0], [np.sin(t), np.cos(t), 0], [0, 0, 1]])
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_ground_truth_fk(gt, pr2, with_base):
+    m = O.OracleMech(pr2, with_base=with_base)
+    jids = [pr2.joint_id(n) for n in gt["joint_names"]]
+    angles = list(gt["angle_vector"]) + ([0.3, 0.3, 0.3] if with_base else [])
+    m.set_joint_angles(jids, angles)
+    for _ in range(2):  # twice: cached values must equal fresh ones (test_kinematics.jl:21)
+        for ln, pg in zip(gt["link_names"], gt["pose_list"]):
+            T = m.get_transform(pr2.link_id(ln))
+            pg = np.asarray(pg)
+            r = O.rpy(T)
+            ypr = np.array([r[2], r[1], r[0]])
+            if with_base:
+                np.testing.assert_allclose(T[:3, 3], _rotz(0.3) @ pg[:3] + [0.3, 0.3, 0], atol=1e-12)
+                np.testing.assert_allclose(ypr, pg[3:] + [0.3, 0, 0], atol=1e-12)
+            else:
+                np.testing.assert_allclose(T[:3, 3], pg[:3], atol=1e-12)
+                np.testing.assert_allclose(ypr, pg[3:], atol=1e-12)
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_fd_jacobian_all_links(gt, pr2, with_base):
+    """test/test_kinematics.jl:43-73, every link, fixture angles and zeros."""
+    m = O.OracleMech(pr2, with_base=with_base)
+    jids = [pr2.joint_id(n) for n in gt["joint_names"]]
+    a1 = np.array(list(gt["angle_vector"]) + ([0.3, 0.3, 0.3] if with_base else []))
+    eps = 1e-7
+    for angles in (a1, a1 * 0):
+        for lid in range(1, len(pr2.link_names) + 1):
+            m.set_joint_angles(jids, angles)
+            Ja = m.get_jacobian(lid, jids, with_rot=True, rpy_jac=True)
+            T0 = m.get_transform(lid)
+            Jn = np.zeros_like(Ja)
+            for i in range(len(angles)):
+                a = angles.copy()
+                a[i] += eps
+                m.set_joint_angles(jids, a)
+                T1 = m.get_transform(lid)
+                Jn[:3, i] = (T1[:3, 3] - T0[:3, 3]) / eps
+                Jn[3:, i] = (O.rpy(T1) - O.rpy(T0)) / eps
+            np.testing.assert_allclose(Jn[:3], Ja[:3], atol=1e-5)
+            if np.linalg.norm(Jn[3:, -3:]) < 1e4:
+                np.testing.assert_allclose(Jn[3:], Ja[3:], atol=1e-5)
+
+
+def test_fetch_mechanism_facts(fetch):
+    """test/test_mechanism.jl:3-29, 54-67 on the oracle tree."""
+    t = fetch
+    base = t.link_id("base_link")
+    kids = {t.link_names[t.joint_clink[j] - 1] for j in range(len(t.joint_names)) if t.joint_plink[j] == base}
+    assert kids == {"r_wheel_link", "l_wheel_link", "torso_lift_link", "estop_link", "laser_link", "torso_fixed_link"}
+    assert base not in set(t.joint_clink)
+    sp = t.link_id("shoulder_pan_link")
+    pj = [j for j in range(len(t.joint_names)) if t.joint_clink[j] == sp]
+    assert t.joint_names[pj[0]] == "shoulder_pan_joint"
+    assert t.link_names[t.joint_plink[pj[0]] - 1] == "torso_lift_link"
+    for leaf in ["r_wheel_link", "l_wheel_link", "r_gripper_finger_link", "l_gripper_finger_link", "bellows_link2",
+                 "estop_link", "laser_link", "torso_fixed_link", "head_camera_rgb_optical_frame",
+                 "head_camera_depth_optical_frame"]:
+        assert t.link_id(leaf) not in set(t.joint_plink)
+    m = O.OracleMech(t)
+    jid = t.joint_id
+    assert m.is_relevant(jid("torso_lift_joint"), t.link_id("torso_lift_link"))
+    assert m.is_relevant(jid("shoulder_pan_joint"), t.link_id("wrist_roll_link"))
+    assert not m.is_relevant(jid("shoulder_pan_joint"), base)
+    new = m.add_new_link(t.link_id("wrist_roll_link"), np.eye(4))
+    assert new == len(t.link_names) + 1
+    assert m.is_relevant(jid("torso_lift_joint"), new)
+
+
+def test_pr2_fragment_rptable(pr2):
+    m = O.OracleMech(pr2)
+    assert m.is_relevant(pr2.joint_id("torso_lift_joint"), pr2.link_id("torso_lift_link"))
+    assert not m.is_relevant(pr2.joint_id("r_wrist_flex_joint"), pr2.link_id("r_elbow_flex_link"))
+
+
+def test_oracle_vs_numpy(fetch):
+    ids = [fetch.joint_id(n) for n in ARM]
+    rng = np.random.default_rng(1)
+    for wb in (False, True):
+        q = rng.uniform(-2, 2, (len(ids) + (3 if wb else 0), 300))
+        m = O.OracleMech(fetch, with_base=wb)
+        gl = fetch.link_id("gripper_link")
+        for rpyj in (False, True):
+            pose, jac = m.fk_jac_batch(q, ids, gl, ids, True, rpyj)
+            T, Jm = R.jacobian(fetch, q, ids, gl, ids, True, rpyj, wb)
+            np.testing.assert_allclose(pose, R.pose12(T), atol=1e-12)
+            np.testing.assert_allclose(jac, Jm.transpose(2, 1, 0), atol=1e-11)
+
+
+def test_golden_fixture_reproduced(fetch):
+    g = np.load(golden("fetch_fk_jac_golden.npz"))
+    ids = [fetch.joint_id(n) for n in g["joint_names"]]
+    m = O.OracleMech(fetch)
+    poses = m.fk_batch(g["q"], ids, list(range(1, len(fetch.link_names) + 1)))
+    np.testing.assert_array_equal(poses, g["poses"])
+    gl = fetch.link_id("gripper_link")
+    _, jg = m.fk_jac_batch(g["q"], ids, gl, ids, True, False)
+    np.testing.assert_array_equal(jg, g["jac_geo"])
+    # sanity derived in SURVEY.md 8c(5): gripper_link at q = 0
+    m0 = O.OracleMech(fetch)
+    np.testing.assert_allclose(m0.get_transform(gl)[:3, 3], [1.1281, 0, 0.78601], atol=1e-12)
+
+
+def test_get_jacobian_bang_leaves_untouched(fetch):
+    """get_jacobian! writes only relevant columns (src/algorithm.jl:91-96)."""
+    m = O.OracleMech(fetch)
+    ids = [fetch.joint_id(n) for n in ARM] + [fetch.joint_id("head_pan_joint")]
+    buf = np.full((6, len(ids)), 7.0)
+    J = m.get_jacobian(fetch.link_id("gripper_link"), ids, True, False, mat=buf)
+    assert np.all(J[:, -1] == 7.0)               # head_pan irrelevant to the gripper
+    assert np.all(J[3:, 0] == 7.0)               # torso is prismatic: rows 4:6 untouched
+    with pytest.raises(ValueError):              # relevant fixed joint -> MethodError
+        m.get_jacobian(fetch.link_id("gripper_link"), [fetch.joint_id("gripper_axis")], True)
+
+
+def test_ik_dls_oracle_reference_target(fetch):
+    """test/test_inverse_kinematics.jl:1-25 acceptance, via the build-defined DLS."""
+    ids = [fetch.joint_id(n) for n in ARM]
+    gl = fetch.link_id("gripper_link")
+    m = O.OracleMech(fetch)
+    T = np.eye(4)
+    T[:3, 3] = [0.3, -0.4, 1.2]
+    tgt = T[:3, :4].T.reshape(12, 1)
+    q, it, err = m.ik_dls_batch(np.zeros((8, 1)), ids, gl, tgt, max_iters=200, tol_pos=1e-4, tol_rot=1e-4)
+    assert it[0] < 200
+    m.set_joint_angles(ids, q[:, 0])
+    Tn = m.get_transform(gl)
+    np.testing.assert_allclose(Tn[:3, 3], T[:3, 3], atol=1e-3)
+    np.testing.assert_allclose(O.rpy(Tn), O.rpy(T), atol=1e-3)
+
+
+def test_nakamura_oracle_reaches_point(fetch):
+    ids = [fetch.joint_id(n) for n in ARM]
+    gl = fetch.link_id("gripper_link")
+    m = O.OracleMech(fetch)
+    target = np.array([0.7, 0.2, 0.9])
+    q = m.point_ik_nakamura(gl, ids, target)
+    m.set_joint_angles(ids, q)
+    assert np.linalg.norm(m.get_transform(gl)[:3, 3] - target) < 1e-3
+
+
+def test_ik_objective_gradient(fetch):
+    """f_objective (src/inverse_kinematics.jl:38-50): grad = -2 J_rpy^T diff vs finite differences."""
+    ids = [fetch.joint_id(n) for n in ARM]
+    gl = fetch.link_id("gripper_link")
+    m = O.OracleMech(fetch)
+    T = np.eye(4)
+    T[:3, 3] = [0.5, -0.2, 1.0]
+    a = np.array([0.1, 0.2, -0.3, 0.4, 0.5, -0.6, 0.3, 0.2])
+    f0, g = m.ik_objective(gl, ids, T, a)
+    eps = 1e-7
+    for i in range(8):
+        b = a.copy()
+        b[i] += eps
+        f1, _ = m.ik_objective(gl, ids, T, b)
+        assert abs((f1 - f0) / eps - g[i]) < 1e-4
