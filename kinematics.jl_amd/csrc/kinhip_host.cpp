@@ -72,6 +72,14 @@ M34 m_from_col16(const double* T) {
     return m;
 }
 
+M34 m_rigid_inverse(const M34& a) {  // [R t]^-1 = [R^T  -R^T t]
+    M34 m{};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) m.r[3 * i + j] = a.r[3 * j + i];
+    for (int i = 0; i < 3; ++i) m.t[i] = -(m.r[3 * i] * a.t[0] + m.r[3 * i + 1] * a.t[1] + m.r[3 * i + 2] * a.t[2]);
+    return m;
+}
+
 M34 m_rot_transpose(const M34& a) {  // inverse of a pure rotation
     M34 m{};
     for (int i = 0; i < 3; ++i)
@@ -560,7 +568,7 @@ struct Stager {
         int block = 256;
         while (block > 64 && (size_t)n_slots * 12 * block * esz > 64 * 1024) block /= 2;
         P.geom.block = block;
-        P.geom.lds = (size_t)n_slots * 12 * block * esz;
+        P.geom.lds = (size_t)n_slots * 12 * block * esz;  // per-lane branch slots
         P.geom.maxA = nA;
         auto fill = [&](auto& K, auto* host) {
             using T = std::remove_reference_t<decltype(host[0].F[0])>;

@@ -21,7 +21,12 @@
 // HBM-bound at the sizes of BASELINE.json (roofline).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kinhip_internal.h"
+
+
+
 
 namespace kinhip {
 namespace {
@@ -93,6 +98,36 @@ __device__ __forceinline__ double atan2_t(double y, double x) { return atan2(y, 
 __device__ __forceinline__ float sqrt_t(float x) { return sqrtf(x); }
 __device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
 
+// SoA addressing: element `row` of a [rows][ld] array for this lane.  Each
+// row gets a wave-uniform buffer descriptor (SGPRs: base = row pointer) and
+// every load/store uses the same 32-bit lane byte offset (one VGPR), i.e.
+// `buffer_load/store_dword v, v_off, s[rsrc], 0 offen` -- no 64-bit per-access
+// address arithmetic in VGPRs.  The launcher splits batches (kChunk) so lane
+// byte offsets stay below 2^31.  KINHIP_STORE_AUX selects the cache policy of
+// the output stream (0 = default, 2 = nt: +10% on the FK+J stream, A/B in
+// profiles/r01_ab_variants.txt).
+#ifndef KINHIP_STORE_AUX
+#define KINHIP_STORE_AUX 2
+#endif
+typedef unsigned int u32x2 __attribute__((__vector_size__(8)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float ld_soa(const float* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base + row * ld), (int)off, 0, 0));
+}
+__device__ __forceinline__ double ld_soa(const double* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base + row * ld), (int)off, 0, 0));
+}
+__device__ __forceinline__ void st_soa(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base + row * ld), (int)off, 0, KINHIP_STORE_AUX);
+}
+__device__ __forceinline__ void st_soa(double* __restrict__ base, int64_t row, int64_t ld, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), row_rsrc(base + row * ld), (int)off, 0,
+                                          KINHIP_STORE_AUX);
+}
+
 template <typename T>
 __device__ __forceinline__ void set_identity(Fr<T>& f) {
 #pragma unroll
@@ -163,13 +198,30 @@ __device__ __forceinline__ void base_frame(Fr<T>& f, T bx, T by, T th) {  // src
     f.t[0] = bx; f.t[1] = by;
 }
 
-// 3x4 column-major SoA store (k = row + 3*col)
+// Output sink: runs of consecutive SoA rows of one array (a pose = 12 rows, a
+// Jacobian column = 6 or 3 rows) for this lane's configuration, one 4/8-byte
+// store per row.  (A 16-byte-per-lane variant staged through LDS measured 5%
+// slower: this stream runs at the ceiling of its access pattern, see
+// profiles/r01_store_probe.txt.)
 template <typename T>
-__device__ __forceinline__ void store_pose(T* __restrict__ dst, int64_t ld, const Fr<T>& L) {
-    dst[0 * ld] = L.r[0]; dst[1 * ld] = L.r[3]; dst[2 * ld] = L.r[6];
-    dst[3 * ld] = L.r[1]; dst[4 * ld] = L.r[4]; dst[5 * ld] = L.r[7];
-    dst[6 * ld] = L.r[2]; dst[7 * ld] = L.r[5]; dst[8 * ld] = L.r[8];
-    dst[9 * ld] = L.t[0]; dst[10 * ld] = L.t[1]; dst[11 * ld] = L.t[2];
+struct Sink {
+    uint32_t off;  // lane byte offset
+
+    template <int NR>
+    __device__ __forceinline__ void rows(T* __restrict__ base, int64_t row0, int64_t ld, const T (&v)[NR],
+                                         int nvalid) const {
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k < nvalid) st_soa(base, row0 + k, ld, off, v[k]);
+    }
+};
+
+// 3x4 column-major pose (k = row + 3*col) of output `o`: rows o*12 .. o*12+11
+template <typename T>
+__device__ __forceinline__ void store_pose(const Sink<T>& sk, T* __restrict__ poses, int64_t o, int64_t ld,
+                                           const Fr<T>& L) {
+    const T v[12] = {L.r[0], L.r[3], L.r[6], L.r[1], L.r[4], L.r[7], L.r[2], L.r[5], L.r[8], L.t[0], L.t[1], L.t[2]};
+    sk.rows(poses, o * 12, ld, v, 12);
 }
 
 template <typename T>
@@ -213,6 +265,51 @@ __device__ __forceinline__ void step_a(Fr<T>& f, const KStep<T>& st, T qv, T (&o
     motion(f, st.kind, st.flags, sc, qv);
 }
 
+// One get_jacobian! column (src/algorithm.jl:65-81): revolute -> [z x (p - o); z or
+// rpy_derivative!(z)], prismatic -> [z; untouched (zeros with get_jacobian)].
+// Written to every column in the step's colmask.
+template <typename T>
+struct JacCtx {
+    T* jac;
+    int64_t ldj;
+    const Sink<T>* sink;
+    int rows;
+    bool with_rot, zero, rpy;
+    T px, py, pz;
+    T k11, k12, k21, k22, k31, k32;  // rpy_derivative! coefficients
+};
+
+template <typename T>
+__device__ __forceinline__ void emit_jcol(const JacCtx<T>& J, const KStep<T>& st, T ox, T oy, T oz, T zx, T zy,
+                                          T zz) {
+    T lin[3], ang[3];
+    const bool prism = st.jkind == MOT_PRISM;
+    if (prism) {
+        lin[0] = zx; lin[1] = zy; lin[2] = zz;
+        ang[0] = ang[1] = ang[2] = T(0);
+    } else {
+        const T dx = J.px - ox, dy = J.py - oy, dz = J.pz - oz;
+        lin[0] = fma(zy, dz, -(zz * dy));
+        lin[1] = fma(zz, dx, -(zx * dz));
+        lin[2] = fma(zx, dy, -(zy * dx));
+        if (J.rpy) {
+            ang[0] = fma(J.k11, zx, J.k12 * zy);
+            ang[1] = fma(J.k21, zx, J.k22 * zy);
+            ang[2] = fma(J.k31, zx, fma(J.k32, zy, zz));
+        } else {
+            ang[0] = zx; ang[1] = zy; ang[2] = zz;
+        }
+    }
+    const T v[6] = {lin[0], lin[1], lin[2], ang[0], ang[1], ang[2]};
+    const int nv = (J.with_rot && (!prism || J.zero)) ? 6 : 3;
+    uint64_t m = st.colmask;
+    while (m) {
+        const int c = __builtin_ctzll(m);
+        m &= m - 1;
+        J.sink->rows(J.jac, (int64_t)c * J.rows, J.ldj, v, nv);
+    }
+}
+
 // --------------------------------------------------------------------------
 // k_fk: batched get_transform (any set of links) + get_jacobian! of one link
 // --------------------------------------------------------------------------
@@ -224,28 +321,34 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* slots = reinterpret_cast<T*>(smem);
     const int B = blockDim.x, tid = threadIdx.x;
-    const int64_t i = (int64_t)blockIdx.x * B + tid;
-    if (i >= n) return;  // no block-wide barrier below: LDS slots are per lane
+    const uint32_t i = blockIdx.x * (uint32_t)B + tid;
+    if (i >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
+    const uint32_t off = i * (uint32_t)sizeof(T);
+    Sink<T> sk;
+    sk.off = off;
 
     const bool base = (P.flags & PF_BASE) != 0;
     T bx = T(0), by = T(0), bth = T(0);
     if (base) {
-        bx = q[(int64_t)P.base_col * ldq + i];
-        by = q[(int64_t)(P.base_col + 1) * ldq + i];
-        bth = q[(int64_t)(P.base_col + 2) * ldq + i];
+        bx = ld_soa(q, P.base_col, ldq, off);
+        by = ld_soa(q, P.base_col + 1, ldq, off);
+        bth = ld_soa(q, P.base_col + 2, ldq, off);
     }
     // every phase-A angle load issued up front (independent, coalesced)
     T qa[MAXA];
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        qa[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+        qa[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
     }
     Fr<T> root;
     if (base) base_frame(root, bx, by, bth);
     else set_identity(root);
 
     Fr<T> f = root;
+    // pre-motion world origin / axis of every phase-A joint, kept in registers
+    // (a register-lighter form that re-derives them backwards with F^-1 measured
+    // 20% slower: more VALU, profiles/r01_ab_variants.txt)
     T ro[MAXA][3], rz[MAXA][3];
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
@@ -254,7 +357,7 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
         if (st.out >= 0) {
             Fr<T> L;
             link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
-            store_pose(poses + (int64_t)st.out * 12 * ldp + i, ldp, L);
+            store_pose(sk, poses, st.out, ldp, L);
         }
         if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
     }
@@ -262,16 +365,16 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
     if ((P.flags & PF_JAC) || P.spine_out >= 0) {
         Fr<T> L;
         link_frame(L, f, P.last_has_x != 0, P.Xlast);
-        if (P.spine_out >= 0) store_pose(poses + (int64_t)P.spine_out * 12 * ldp + i, ldp, L);
+        if (P.spine_out >= 0) store_pose(sk, poses, P.spine_out, ldp, L);
         if (P.flags & PF_JAC) {
-            const T px = L.t[0], py = L.t[1], pz = L.t[2];
-            const int rows = P.rows;
-            const bool with_rot = (P.flags & PF_WITH_ROT) != 0;
-            const bool zero = (P.flags & PF_ZERO) != 0;
-            // rpy_derivative! coefficients (src/algorithm.jl:56-63) from RotZYX(L)
-            T k11 = 0, k12 = 0, k21 = 0, k22 = 0, k31 = 0, k32 = 0;
-            const bool rpy = with_rot && (P.flags & PF_RPY);
-            if (rpy) {
+            JacCtx<T> J;
+            J.jac = jac; J.ldj = ldj; J.sink = &sk; J.rows = P.rows;
+            J.with_rot = (P.flags & PF_WITH_ROT) != 0;
+            J.zero = (P.flags & PF_ZERO) != 0;
+            J.rpy = J.with_rot && (P.flags & PF_RPY);
+            J.px = L.t[0]; J.py = L.t[1]; J.pz = L.t[2];
+            J.k11 = J.k12 = J.k21 = J.k22 = J.k31 = J.k32 = T(0);
+            if (J.rpy) {  // rpy_derivative! coefficients (src/algorithm.jl:56-63) from RotZYX(L)
                 const T t1 = atan2_t(L.r[3], L.r[0]);
                 T st1, ct1;
                 sincos_t(t1, &st1, &ct1);
@@ -279,66 +382,32 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
                 T s2, c2, s3, c3;
                 sincos_t(-t2, &s2, &c2);
                 sincos_t(-t1, &s3, &c3);
-                k11 = c3 / c2; k12 = -(s3 / c2);
-                k21 = s3; k22 = c3;
-                k31 = -(c3 * s2 / c2); k32 = s3 * s2 / c2;
+                J.k11 = c3 / c2; J.k12 = -(s3 / c2);
+                J.k21 = s3; J.k22 = c3;
+                J.k31 = -(c3 * s2 / c2); J.k32 = s3 * s2 / c2;
             }
 #pragma unroll
-            for (int s = 0; s < MAXA; ++s) {
-                if (S[s].flags & SF_REC) {
-                    const T zx = rz[s][0], zy = rz[s][1], zz = rz[s][2];
-                    T lin[3], ang[3];
-                    const bool prism = S[s].jkind == MOT_PRISM;
-                    if (prism) {
-                        lin[0] = zx; lin[1] = zy; lin[2] = zz;
-                        ang[0] = ang[1] = ang[2] = T(0);
-                    } else {
-                        const T dx = px - ro[s][0], dy = py - ro[s][1], dz = pz - ro[s][2];
-                        lin[0] = fma(zy, dz, -(zz * dy));
-                        lin[1] = fma(zz, dx, -(zx * dz));
-                        lin[2] = fma(zx, dy, -(zy * dx));
-                        if (rpy) {
-                            ang[0] = fma(k11, zx, k12 * zy);
-                            ang[1] = fma(k21, zx, k22 * zy);
-                            ang[2] = fma(k31, zx, fma(k32, zy, zz));
-                        } else {
-                            ang[0] = zx; ang[1] = zy; ang[2] = zz;
-                        }
-                    }
-                    uint64_t m = S[s].colmask;
-                    while (m) {
-                        const int c = __builtin_ctzll(m);
-                        m &= m - 1;
-                        T* col = jac + (int64_t)c * rows * ldj + i;
-                        col[0] = lin[0]; col[ldj] = lin[1]; col[2 * ldj] = lin[2];
-                        if (with_rot && (!prism || zero)) {
-                            col[3 * ldj] = ang[0]; col[4 * ldj] = ang[1]; col[5 * ldj] = ang[2];
-                        }
-                    }
-                }
-            }
-            if (zero) {
+            for (int s = 0; s < MAXA; ++s)
+                if (S[s].flags & SF_REC) emit_jcol(J, S[s], ro[s][0], ro[s][1], ro[s][2], rz[s][0], rz[s][1], rz[s][2]);
+            const int rows = P.rows;
+            if (J.zero) {
+                const T z6[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
                 uint64_t m = P.zmask;
                 while (m) {
                     const int c = __builtin_ctzll(m);
                     m &= m - 1;
-                    T* col = jac + (int64_t)c * rows * ldj + i;
-                    for (int r = 0; r < rows; ++r) col[r * ldj] = T(0);
+                    sk.rows(jac, (int64_t)c * rows, ldj, z6, rows);
                 }
             }
             if (base) {  // src/algorithm.jl:98-105
-                const T x = px - bx, y = py - by;
-                T* c0 = jac + (int64_t)P.n_jac * rows * ldj + i;
-                T* c1 = c0 + (int64_t)rows * ldj;
-                T* c2 = c1 + (int64_t)rows * ldj;
-                c0[0] = T(1); c0[ldj] = T(0); c0[2 * ldj] = T(0);
-                c1[0] = T(0); c1[ldj] = T(1); c1[2 * ldj] = T(0);
-                c2[0] = -y; c2[ldj] = x; c2[2 * ldj] = T(0);
-                if (with_rot) {
-                    c0[3 * ldj] = T(0); c0[4 * ldj] = T(0); c0[5 * ldj] = T(0);
-                    c1[3 * ldj] = T(0); c1[4 * ldj] = T(0); c1[5 * ldj] = T(0);
-                    c2[3 * ldj] = T(0); c2[4 * ldj] = T(0); c2[5 * ldj] = T(1);
-                }
+                const T x = J.px - bx, y = J.py - by;
+                const int64_t b0 = (int64_t)P.n_jac * rows;
+                const T c0[6] = {T(1), T(0), T(0), T(0), T(0), T(0)};
+                const T c1[6] = {T(0), T(1), T(0), T(0), T(0), T(0)};
+                const T c2[6] = {-y, x, T(0), T(0), T(0), T(1)};
+                sk.rows(jac, b0, ldj, c0, rows);
+                sk.rows(jac, b0 + rows, ldj, c1, rows);
+                sk.rows(jac, b0 + 2 * rows, ldj, c2, rows);
             }
         }
     }
@@ -350,11 +419,11 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
         if (ld == LOAD_ROOT) f = root;
         else if (ld >= 0) slot_load(slots, ld, B, tid, f);
         mul_rigid(f, st.F);
-        if (st.kind != MOT_NONE) motion(f, st.kind, st.flags, st.scale, q[(int64_t)st.qcol * ldq + i]);
+        if (st.kind != MOT_NONE) motion(f, st.kind, st.flags, st.scale, ld_soa(q, st.qcol, ldq, off));
         if (st.out >= 0) {
             Fr<T> L;
             link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
-            store_pose(poses + (int64_t)st.out * 12 * ldp + i, ldp, L);
+            store_pose(sk, poses, st.out, ldp, L);
         }
         if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
     }
@@ -439,25 +508,26 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
                                                 T* __restrict__ q, int64_t ldq, int64_t n,
                                                 int32_t* __restrict__ iters, T* __restrict__ err,
                                                 int64_t lde) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)n) return;
+    const uint32_t off = i * (uint32_t)sizeof(T);
     T Rt[9], pt[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) Rt[3 * r + c] = tgt[(int64_t)(r + 3 * c) * ldt + i];
-        pt[r] = tgt[(int64_t)(9 + r) * ldt + i];
+        for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
+        pt[r] = ld_soa(tgt, 9 + r, ldt, off);
     }
     T qs[MAXA];
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        qs[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+        qs[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
     }
     const bool base = (P.flags & PF_BASE) != 0;
     T b[3] = {T(0), T(0), T(0)};
     if (base)
-        for (int k = 0; k < 3; ++k) b[k] = q[(int64_t)(P.base_col + k) * ldq + i];
+        for (int k = 0; k < 3; ++k) b[k] = ld_soa(q, P.base_col + k, ldq, off);
 
     int it = 0;
     T ep = 0, er = 0;
@@ -594,14 +664,14 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        if (c >= 0) q[(int64_t)c * ldq + i] = qs[s];
+        if (c >= 0) st_soa(q, c, ldq, off, qs[s]);
     }
     if (base)
-        for (int k = 0; k < 3; ++k) q[(int64_t)(P.base_col + k) * ldq + i] = b[k];
+        for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
     if (iters) iters[i] = it;
     if (err) {
-        err[i] = ep;
-        err[lde + i] = er;
+        st_soa(err, 0, lde, off, ep);
+        st_soa(err, 1, lde, off, er);
     }
 }
 
@@ -612,14 +682,15 @@ template <typename T, int MAXA>
 __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                   const T* __restrict__ pts, int64_t ldpt, T* __restrict__ q,
                                                   int64_t ldq, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const T pd0 = pts[i], pd1 = pts[ldpt + i], pd2 = pts[2 * ldpt + i];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)n) return;
+    const uint32_t off = i * (uint32_t)sizeof(T);
+    const T pd0 = ld_soa(pts, 0, ldpt, off), pd1 = ld_soa(pts, 1, ldpt, off), pd2 = ld_soa(pts, 2, ldpt, off);
     T qs[MAXA];
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        qs[s] = c >= 0 ? q[(int64_t)c * ldq + i] : T(0);
+        qs[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
     }
     Fr<T> root;
     set_identity(root);
@@ -657,7 +728,7 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        if (c >= 0) q[(int64_t)c * ldq + i] = qs[s];
+        if (c >= 0) st_soa(q, c, ldq, off, qs[s]);
     }
 }
 
@@ -675,48 +746,74 @@ inline unsigned grid_of(int64_t n, int block) { return (unsigned)((n + block - 1
     default: CALL(32); break;      \
     }
 
+// Launches are split into chunks of kChunk configurations so that every lane
+// byte offset (uint32, ld_soa / st_soa) fits in 32 bits; chunks are pointer
+// offsets into the same SoA arrays (the leading dimensions do not change).
+constexpr int64_t kChunk = int64_t(1) << 27;
+
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
                      int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    const dim3 grid(grid_of(n, g.block)), block(g.block);
+    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        const int64_t c = std::min(kChunk, n - s0);
+        const dim3 grid(grid_of(c, g.block)), block(g.block);
+        const T* qc = q ? q + s0 : q;
+        T* pc = poses ? poses + s0 : poses;
+        T* jc = jac ? jac + s0 : jac;
 #define KIN_FK_LAUNCH(MA) \
-    hipLaunchKernelGGL((k_fk<T, MA>), grid, block, g.lds, st, P, steps, q, ldq, n, poses, ldp, jac, ldj)
-    KIN_MAXA_DISPATCH(g.maxA, KIN_FK_LAUNCH)
+        hipLaunchKernelGGL((k_fk<T, MA>), grid, block, g.lds, st, P, steps, qc, ldq, c, pc, ldp, jc, ldj)
+        KIN_MAXA_DISPATCH(g.maxA, KIN_FK_LAUNCH)
 #undef KIN_FK_LAUNCH
-    return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
                          int64_t lde, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step)};
-    const dim3 grid(grid_of(n, 256)), block(256);
+    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        const int64_t c = std::min(kChunk, n - s0);
+        const dim3 grid(grid_of(c, 256)), block(256);
+        const T* tc = target + s0;
+        T* qc = q + s0;
+        int32_t* ic = iters ? iters + s0 : iters;
+        T* ec = err ? err + s0 : err;
 #define KIN_IK6(MA) \
-    hipLaunchKernelGGL((k_ik_dls<T, MA, 6>), grid, block, 0, st, P, steps, at, target, ldt, q, ldq, n, iters, err, lde)
+        hipLaunchKernelGGL((k_ik_dls<T, MA, 6>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
 #define KIN_IK3(MA) \
-    hipLaunchKernelGGL((k_ik_dls<T, MA, 3>), grid, block, 0, st, P, steps, at, target, ldt, q, ldq, n, iters, err, lde)
-    if (a.with_rot) {
-        KIN_MAXA_DISPATCH(g.maxA, KIN_IK6)
-    } else {
-        KIN_MAXA_DISPATCH(g.maxA, KIN_IK3)
-    }
+        hipLaunchKernelGGL((k_ik_dls<T, MA, 3>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
+        if (a.with_rot) {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_IK6)
+        } else {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_IK3)
+        }
 #undef KIN_IK6
 #undef KIN_IK3
-    return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
                            int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st) {
-    if (n <= 0) return hipSuccess;
-    const dim3 grid(grid_of(n, 256)), block(256);
-#define KIN_NK_LAUNCH(MA) hipLaunchKernelGGL((k_nakamura<T, MA>), grid, block, 0, st, P, steps, pts, ldpt, q, ldq, n)
-    KIN_MAXA_DISPATCH(g.maxA, KIN_NK_LAUNCH)
+    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        const int64_t c = std::min(kChunk, n - s0);
+        const dim3 grid(grid_of(c, 256)), block(256);
+        const T* pc = pts + s0;
+        T* qc = q + s0;
+#define KIN_NK_LAUNCH(MA) hipLaunchKernelGGL((k_nakamura<T, MA>), grid, block, 0, st, P, steps, pc, ldpt, qc, ldq, c)
+        KIN_MAXA_DISPATCH(g.maxA, KIN_NK_LAUNCH)
 #undef KIN_NK_LAUNCH
-    return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 #define KIN_INSTANTIATE(T)                                                                                    \

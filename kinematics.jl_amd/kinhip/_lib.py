@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede the HIP library: shared runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libkinhip.so"))
+LIB_PATH = os.environ.get("KINHIP_LIB") or os.path.normpath(os.path.join(_HERE, "..", "lib", "libkinhip.so"))
 
 KIN_OK = 0
 KIN_E_INVALID, KIN_E_KEY, KIN_E_METHOD, KIN_E_DEVICE = -1, -2, -3, -4

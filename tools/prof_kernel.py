@@ -1,0 +1,47 @@
+"""Runs one engine workload K times for rocprofv3 (kernel trace / PMC passes).
+
+    python tools/prof_kernel.py --what fkjac32 --steps 20
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
+import kinhip  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac64", "fk6_64", "ik32", "ik64"])
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--n", type=int, default=1 << 20)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
+gl = m.find_link("gripper_link")
+dt = torch.float64 if a.what.endswith("64") else torch.float32
+Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], a.n, dtype=dt, device=dev)
+if a.what.startswith("fkjac"):
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    P = torch.empty((1, 12, a.n), dtype=dt, device=dev)
+    J = torch.empty((8, 6, a.n), dtype=dt, device=dev)
+    for _ in range(a.steps):
+        plan.run(Q, P, J)
+elif a.what == "fk6_64":
+    links = [m.find_link(n) for n in ["l_gripper_finger_link", "r_gripper_finger_link", "wrist_flex_link",
+                                      "wrist_roll_link", "shoulder_lift_link", "upperarm_roll_link"]]
+    plan = m.plan(arm, out_links=links, dtype=dt)
+    P = torch.empty((6, 12, a.n), dtype=dt, device=dev)
+    for _ in range(a.steps):
+        plan.run(Q, P)
+else:
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    T, _ = plan.run(Q)
+    tgt = T[0].contiguous()
+    for _ in range(a.steps):
+        Q0 = torch.zeros_like(Q)
+        plan.ik_dls(tgt, Q0, max_iters=64)
+torch.cuda.synchronize()
+print("done", a.what, a.steps)

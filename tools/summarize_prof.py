@@ -1,0 +1,84 @@
+"""Summarise rocprofv3 outputs under gpurun_out/prof into committed profiles/ files.
+
+HBM bytes per launch follow MI355X_MICROARCH.md (HBM / rocprofv3 section):
+FETCH_SIZE and WRITE_SIZE are in KB; on gfx950 FETCH_SIZE reports half of the
+bytes of a coalesced streaming read, so hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+
+    python tools/summarize_prof.py --round r01
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "gpurun_out", "prof")
+OUT = os.path.join(ROOT, "profiles")
+
+WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
+    "fkjac32": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20), "FK + 6x8 J, fp32, N = 2^20: 8 q in, 60 out"),
+    "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
+    "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
+}
+
+
+def counters(tag):
+    agg = collections.defaultdict(list)
+    kern = WORK[tag][0]
+    for f in glob.glob(os.path.join(PROF, f"{tag}_*", "*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def stats(path, kern):
+    for r in csv.DictReader(open(path)):
+        if kern in r["Name"]:
+            return {k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "StdDev")}
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", default="r01")
+    a = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    for tag, (kern, alg, note) in WORK.items():
+        c = counters(tag)
+        if not c:
+            continue
+        st = None
+        for p in glob.glob(os.path.join(PROF, f"{tag}_trace", "*_kernel_stats.csv")):
+            st = stats(p, kern)
+            shutil.copy(p, os.path.join(OUT, f"{a.round}_{tag}_kernel_stats.csv"))
+        hbm = None
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            hbm = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        d = {"workload": tag, "note": note, "kernel": kern, "round": a.round,
+             "algorithmic_bytes_per_launch": alg, "hbm_bytes_per_launch": hbm,
+             "traffic_over_algorithmic": (hbm / alg) if hbm else None,
+             "fetch_size_kb_raw": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
+             "avg_duration_ns_trace": float(st["AverageNs"]) if st else None,
+             "achieved_GBs_trace": (alg / float(st["AverageNs"])) if st else None,
+             "sq": {k: v for k, v in c.items() if k.startswith(("SQ_", "GRBM_"))},
+             "method": "rocprofv3 --kernel-trace --stats, then separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ_*), "
+                       "20 launches each via tools/prof_kernel.py; hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950)"}
+        with open(os.path.join(OUT, f"{a.round}_pmc_{tag}.json"), "w") as f:
+            json.dump(d, f, indent=1)
+        if tag == "fkjac32":
+            with open(os.path.join(OUT, "pmc_fk_jac_f32.json"), "w") as f:
+                json.dump(d, f, indent=1)
+        print(json.dumps({k: d[k] for k in ("workload", "hbm_bytes_per_launch", "traffic_over_algorithmic",
+                                            "avg_duration_ns_trace", "achieved_GBs_trace")}))
+    b = os.path.join(PROF, "bench", "bench_kernel_stats.csv")
+    if os.path.exists(b):
+        shutil.copy(b, os.path.join(OUT, f"{a.round}_bench_kernel_stats.csv"))
+        print("bench:", stats(b, "k_fk<float, 8>"))
+
+
+if __name__ == "__main__":
+    main()
