@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 
 import kinhip  # noqa: E402
+from kinhip import dist as D  # noqa: E402
 
 ARM = kinhip.FETCH_ARM_JOINTS
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
@@ -33,27 +34,13 @@ EXAMPLE_LINKS = ["l_gripper_finger_link", "r_gripper_finger_link", "wrist_flex_l
                  "shoulder_lift_link", "upperarm_roll_link"]
 
 
-def _dist():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        return dist, rank, ws, local
-    torch.cuda.set_device(local)
-    return None, rank, ws, local
-
-
-def _time_plan(plan, Q, poses, jac, steps, warmup, dist, stream):
+def _time_plan(plan, Q, poses, jac, steps, warmup, ctx, stream):
     """K back-to-back launches bracketed by barrier + synchronize; HIP events on the launch stream."""
     with torch.cuda.stream(stream):
         for _ in range(warmup):
             plan.run(Q, poses, jac, stream=stream)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    D.barrier(ctx)
     torch.cuda.synchronize()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -63,15 +50,54 @@ def _time_plan(plan, Q, poses, jac, steps, warmup, dist, stream):
         plan.run(Q, poses, jac, stream=stream)
     e1.record(stream)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    D.barrier(ctx)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     dev_s = e0.elapsed_time(e1) / 1e3
-    t = torch.tensor([wall, dev_s], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0]), float(t[1])
+    wall, dev_s = D.max_over_ranks(ctx, [wall, dev_s])
+    return wall, dev_s
+
+
+def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
+    """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
+    <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
+    Multi-GPU: the solutions (8 angles) and iteration counts are all-gathered to every rank over
+    RCCL afterwards -- timed separately, not part of the solve rate."""
+    dt = torch.float32
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    start, cnt = D.shard_range(n, ctx.rank)
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], cnt, start=start,
+                                seed=4242, dtype=dt, device=ctx.device)
+    tgt = plan.run(Qt)[0][0].contiguous()
+    Q0 = torch.zeros((8, cnt), dtype=dt, device=ctx.device)
+    kw = dict(max_iters=64, restarts=3, seed=ctx.rank, lam=1e-2, max_step=0.5, tol_pos=1e-3, tol_rot=1e-3)
+    with torch.cuda.stream(stream):
+        plan.ik_dls(tgt, Q0.clone(), stream=stream, **kw)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for _ in range(reps):
+            Q = Q0.clone()
+            Q, it, err = plan.ik_dls(tgt, Q, stream=stream, **kw)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    wall = D.max_over_ranks(ctx, [time.perf_counter() - t0])[0]
+    succ = (it < 64).float().mean()
+    out = {"value": n * ctx.world * reps / wall, "unit": "IK solves/s", "targets_per_gpu": n,
+           "success_rate": float(succ), "ms_per_batch": wall / reps * 1e3, "dtype": "f32",
+           "params": "DLS lambda=1e-2, max_step=0.5, 64 iters incl. 3 seeded restarts, q0=0"}
+    if ctx.world > 1:
+        torch.cuda.synchronize()
+        D.barrier(ctx)
+        g0 = time.perf_counter()
+        allq = D.all_gather_cols(ctx, Q)
+        alli = D.all_gather_cols(ctx, it.reshape(1, -1))
+        torch.cuda.synchronize()
+        out["gather_ms"] = D.max_over_ranks(ctx, [(time.perf_counter() - g0) * 1e3])[0]
+        out["gathered_success_rate"] = float((alli < 64).float().mean())
+        assert allq.shape == (8, n * ctx.world)
+    return out
 
 
 def _cpu_baseline(m, N_budget_s=12.0):
@@ -121,8 +147,8 @@ def main():
     ap.add_argument("--extras", type=int, default=1, help="also time fp64 FK+J and config-2 FK")
     args = ap.parse_args()
 
-    dist, rank, ws, local = _dist()
-    dev = torch.device("cuda", local)
+    ctx = D.init_from_env()
+    rank, ws, dev = ctx.rank, ctx.world, ctx.device
     m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
     arm = [m.find_joint(n) for n in ARM]
     gl = m.find_link("gripper_link")
@@ -140,7 +166,7 @@ def main():
 
     # ---- headline: FK + J, fp32 -------------------------------------------------
     plan, Q, poses, J = leg(torch.float32, True, [gl])
-    wall, dev_s = _time_plan(plan, Q, poses, J, args.steps, args.warmup, dist, stream)
+    wall, dev_s = _time_plan(plan, Q, poses, J, args.steps, args.warmup, ctx, stream)
     evals = N * ws * args.steps
     value = evals / wall
     bytes_per_eval = (8 + 12 + 48) * 4  # q in + pose + J out (algorithmic)
@@ -164,24 +190,25 @@ def main():
     if args.extras:
         # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
         p64, Q64, P64, J64 = leg(torch.float64, True, [gl])
-        w64, d64 = _time_plan(p64, Q64, P64, J64, max(5, args.steps // 2), 3, dist, stream)
+        w64, d64 = _time_plan(p64, Q64, P64, J64, max(5, args.steps // 2), 3, ctx, stream)
         out["fp64_fk_jac"] = {"value": N * ws * max(5, args.steps // 2) / w64, "unit": "evals/s",
                               "avg_launch_us": d64 / max(5, args.steps // 2) * 1e6,
                               "achieved_GBs": 544 * N / (d64 / max(5, args.steps // 2)) / 1e9}
         del p64, Q64, P64, J64
         links = [m.find_link(n) for n in EXAMPLE_LINKS]
         p2, Q2, P2, _ = leg(torch.float64, False, links)
-        w2, d2 = _time_plan(p2, Q2, P2, None, max(5, args.steps // 2), 3, dist, stream)
+        w2, d2 = _time_plan(p2, Q2, P2, None, max(5, args.steps // 2), 3, ctx, stream)
         k2 = max(5, args.steps // 2)
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9}
         del p2, Q2, P2
+        out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = _cpu_baseline(m)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    if ctx.dist:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -196,6 +196,10 @@ typedef struct kin_ik_params {
     double tol_rot;     /* |axis-angle error| tolerance, e.g. 1e-3 */
     double max_step;    /* max |dq|_inf per iteration, e.g. 0.5 */
     int32_t with_rot;   /* 0: position only */
+    int32_t restarts;   /* 0: none; else max_iters is split into restarts+1 attempts and each new
+                           attempt re-draws the relevant joints uniformly within their limits
+                           (U[-pi, pi] if unbounded) from a counter hash of (seed, i, attempt, column) */
+    uint64_t seed;
 } kin_ik_params;
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,

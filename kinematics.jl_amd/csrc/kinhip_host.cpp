@@ -846,9 +846,10 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
     if (n == 0) return KIN_OK;
     if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
-    if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0))
+    if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0) || prm->restarts < 0)
         return set_error(KIN_E_INVALID, "bad IK parameters");
-    IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot};
+    IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
+             prm->restarts, prm->seed};
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,

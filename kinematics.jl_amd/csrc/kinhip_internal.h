@@ -23,6 +23,8 @@ struct IkArgs {
     int32_t max_iters;
     double lambda, tol_pos, tol_rot, max_step;
     int32_t with_rot;
+    int32_t restarts;
+    uint64_t seed;
 };
 
 template <typename T>

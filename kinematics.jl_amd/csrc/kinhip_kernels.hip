@@ -497,7 +497,20 @@ template <typename T>
 struct IkArgsT {
     int32_t max_iters;
     T lam2, tol_pos, tol_rot, max_step;
+    int32_t attempt_len;  // 0: no restarts
+    uint64_t seed;
+    int64_t ibase;  // global index of this chunk's first configuration
 };
+
+// restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
+__device__ __forceinline__ double ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col) {
+    const uint64_t key = (uint64_t)i * 131ull + (uint64_t)attempt * 31ull + (uint64_t)col + 1ull;
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * key + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
 
 // --------------------------------------------------------------------------
 // k_ik_dls: batched damped least squares, dq = J^T (J J^T + lambda^2 I)^-1 e
@@ -528,6 +541,7 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
     T b[3] = {T(0), T(0), T(0)};
     if (base)
         for (int k = 0; k < 3; ++k) b[k] = ld_soa(q, P.base_col + k, ldq, off);
+    const T b0[3] = {b[0], b[1], b[2]};
 
     int it = 0;
     T ep = 0, er = 0;
@@ -548,6 +562,20 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
             er = sqrt_t(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
         if ((ep < a.tol_pos && er < a.tol_rot) || it >= a.max_iters) break;
+        if (a.attempt_len > 0 && it > 0 && it % a.attempt_len == 0) {  // restart (see kin_ik_params)
+            const int32_t att = it / a.attempt_len;
+#pragma unroll
+            for (int s = 0; s < MAXA; ++s) {
+                const KStep<T>& st = S[s];
+                if (st.qcol >= 0 && (st.flags & SF_REC)) {
+                    double lo = (double)st.lo, hi = (double)st.hi;
+                    if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
+                    qs[s] = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, a.ibase + (int64_t)i, att, st.qcol));
+                }
+            }
+            for (int k = 0; k < 3; ++k) b[k] = b0[k];
+            continue;
+        }
 
         T Jb[3][ROWS];
         if (base) {
@@ -774,8 +802,10 @@ template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
                          int64_t lde, hipStream_t st) {
-    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step)};
+    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step),
+                  a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0, a.seed, 0};
     for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        at.ibase = s0;
         const int64_t c = std::min(kChunk, n - s0);
         const dim3 grid(grid_of(c, 256)), block(256);
         const T* tc = target + s0;

@@ -1,0 +1,212 @@
+# KinematicsHIP.jl -- Julia-side drop-in for Kinematics.jl's hot path on MI355X.
+#
+# Binds libkinhip.so (include/kinhip.h) with `ccall`.  Keeps the reference's
+# Mechanism / parse_urdf / find_link / set_joint_angles API untouched (they stay
+# in Kinematics.jl) and adds batched methods of the hot-path functions:
+#
+#   get_transform(m, link)                 src/algorithm.jl:1-4     -> get_transform(hm, links, joints, Q)
+#   get_jacobian!(m, link, joints, ...)    src/algorithm.jl:83-106  -> get_jacobian!(hm, link, joints, with_rot, J, Q; rpy_jac)
+#   inverse_kinematics!(m, link, ...)      src/inverse_kinematics.jl:23-30 -> inverse_kinematics!(hm, link, joints, targets, Q)
+#   point_inverse_kinematics_nakamura      src/algorithm.jl:116-131 -> point_inverse_kinematics_nakamura!(hm, link, joints, points, Q)
+#
+# Device arrays are AMDGPU.jl `ROCArray`s in Julia's column-major layout:
+#   Q :: ROCMatrix{T}(N, n_joints [+3 base])      (configuration index fastest)
+#   poses :: ROCArray{T,3}(N, 12, n_links)        (3x4 column-major per link)
+#   J :: ROCArray{T,3}(N, rows, n_cols)           (get_jacobian!'s mat_out per configuration)
+# which is exactly the SoA layout of the C-ABI, so `pointer(A)` is passed
+# zero-copy.  T is Float32 or Float64.
+#
+# NOTE: this file is not executed in the build container (no Julia toolchain);
+# the same C-ABI is exercised by tests/ through Python ctypes.
+module KinematicsHIP
+
+using Kinematics
+using AMDGPU
+
+const libkinhip = joinpath(@__DIR__, "..", "lib", "libkinhip.so")
+
+const KIN_F32 = Int32(0)
+const KIN_F64 = Int32(1)
+const KIN_WITH_ROT = UInt32(1)
+const KIN_RPY_JAC = UInt32(2)
+const KIN_ZERO_FILL = UInt32(4)
+
+struct KinTreeDesc
+    n_links::Int32
+    n_joints::Int32
+    joint_type::Ptr{Int32}
+    joint_plink::Ptr{Int32}
+    joint_clink::Ptr{Int32}
+    joint_pose::Ptr{Float64}
+    joint_axis::Ptr{Float64}
+    joint_lower::Ptr{Float64}
+    joint_upper::Ptr{Float64}
+    with_base::Int32
+end
+
+struct KinPlanDesc
+    dtype::Int32
+    n_q::Int32
+    q_joint_ids::Ptr{Int32}
+    n_out::Int32
+    out_link_ids::Ptr{Int32}
+    jac_link_id::Int32
+    n_jac::Int32
+    jac_joint_ids::Ptr{Int32}
+    jac_flags::UInt32
+end
+
+struct KinIkParams
+    max_iters::Int32
+    lambda::Float64
+    tol_pos::Float64
+    tol_rot::Float64
+    max_step::Float64
+    with_rot::Int32
+    restarts::Int32
+    seed::UInt64
+end
+
+function check(rc::Cint)
+    if rc != 0
+        msg = unsafe_string(ccall((:kin_last_error, libkinhip), Cstring, ()))
+        rc == -2 && throw(KeyError(msg))                   # reference: Dict KeyError
+        rc == -3 && throw(MethodError(joint_jacobian_stub, (msg,)))  # no joint_jacobian! method (fixed joint)
+        error("kinhip error $rc: $msg")
+    end
+    nothing
+end
+joint_jacobian_stub(x) = nothing
+
+joint_type_code(::Kinematics.Joint{Kinematics.Fixed}) = Int32(0)
+joint_type_code(::Kinematics.Joint{Kinematics.Revolute}) = Int32(1)
+joint_type_code(::Kinematics.Joint{Kinematics.Prismatic}) = Int32(2)
+joint_axis(j::Kinematics.Joint{Kinematics.Fixed}) = (1.0, 0.0, 0.0)
+joint_axis(j::Kinematics.Joint) = Tuple(j.jt.axis)
+
+"""HIP-side model of a Mechanism: the tree of `m` (ids as in `m`) and its current `m.angles`
+for joints that batches do not drive.  Re-create after `add_new_link`."""
+mutable struct HIPModel
+    handle::Ptr{Cvoid}
+    m::Mechanism
+    plans::Dict{Any,Ptr{Cvoid}}
+end
+
+function HIPModel(m::Mechanism)
+    J = length(m.joints)
+    jt = Int32[joint_type_code(j) for j in m.joints]
+    jp = Int32[j.plink_id for j in m.joints]
+    jc = Int32[j.clink_id for j in m.joints]
+    pose = Float64[]
+    axis = Float64[]
+    for j in m.joints
+        append!(pose, vec(Matrix(j.pose.mat)))          # column-major 4x4
+        append!(axis, collect(joint_axis(j)))
+    end
+    lo = Float64[Kinematics.lower_limit(j) for j in m.joints]
+    hi = Float64[Kinematics.upper_limit(j) for j in m.joints]
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve jt jp jc pose axis lo hi begin
+        d = KinTreeDesc(length(m.links), J, pointer(jt), pointer(jp), pointer(jc), pointer(pose), pointer(axis),
+                        pointer(lo), pointer(hi), Int32(m.with_base))
+        check(ccall((:kin_model_create, libkinhip), Cint, (Ref{KinTreeDesc}, Ref{Ptr{Cvoid}}), d, h))
+    end
+    check(ccall((:kin_model_set_angles, libkinhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], m.angles))
+    hm = HIPModel(h[], m, Dict{Any,Ptr{Cvoid}}())
+    finalizer(hm) do x
+        for p in values(x.plans)
+            ccall((:kin_plan_destroy, libkinhip), Cint, (Ptr{Cvoid},), p)
+        end
+        ccall((:kin_model_destroy, libkinhip), Cint, (Ptr{Cvoid},), x.handle)
+    end
+    hm
+end
+
+dtype_code(::Type{Float32}) = KIN_F32
+dtype_code(::Type{Float64}) = KIN_F64
+
+function plan!(hm::HIPModel, ::Type{T}, qj, outs, jl, jj, flags) where {T}
+    key = (T, qj, outs, jl, jj, flags)
+    get!(hm.plans, key) do
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        GC.@preserve qj outs jj begin
+            d = KinPlanDesc(dtype_code(T), length(qj), pointer(qj), length(outs), pointer(outs), jl, length(jj),
+                            pointer(jj), flags)
+            check(ccall((:kin_plan_create, libkinhip), Cint, (Ptr{Cvoid}, Ref{KinPlanDesc}, Ref{Ptr{Cvoid}}),
+                        hm.handle, d, h))
+        end
+        h[]
+    end
+end
+
+stream_ptr() = AMDGPU.stream().stream
+
+"""Batched `get_transform`: poses[:, :, k] = world pose (3x4, column-major) of links[k] for every row of Q."""
+function Kinematics.get_transform(hm::HIPModel, links::Vector{<:Link}, joints::Vector{<:Joint},
+                                  Q::ROCMatrix{T}) where {T<:Union{Float32,Float64}}
+    N = size(Q, 1)
+    poses = ROCArray{T}(undef, N, 12, length(links))
+    p = plan!(hm, T, Int32[j.id for j in joints], Int32[l.id for l in links], Int32(0), Int32[], UInt32(0))
+    check(ccall((:kin_plan_run, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
+                p, pointer(Q), stride(Q, 2), N, pointer(poses), N, C_NULL, 0, stream_ptr()))
+    poses
+end
+
+"""Batched `get_jacobian!`: J[i, :, :] is mat_out of configuration i; untouched entries keep their values."""
+function Kinematics.get_jacobian!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool,
+                                  J::ROCArray{T,3}, Q::ROCMatrix{T}; rpy_jac=false,
+                                  pose::Union{Nothing,ROCArray{T,3}}=nothing) where {T<:Union{Float32,Float64}}
+    N = size(Q, 1)
+    flags = (with_rot ? KIN_WITH_ROT : UInt32(0)) | (rpy_jac ? KIN_RPY_JAC : UInt32(0))
+    ids = Int32[j.id for j in joints]
+    outs = pose === nothing ? Int32[] : Int32[link.id]
+    p = plan!(hm, T, ids, outs, Int32(link.id), ids, flags)
+    check(ccall((:kin_plan_run, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
+                p, pointer(Q), stride(Q, 2), N, pose === nothing ? C_NULL : pointer(pose), N, pointer(J), N,
+                stream_ptr()))
+    J
+end
+
+function Kinematics.get_jacobian(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool,
+                                 Q::ROCMatrix{T}; rpy_jac=false) where {T}
+    rows = with_rot ? 6 : 3
+    cols = length(joints) + (hm.m.with_base ? 3 : 0)
+    J = AMDGPU.zeros(T, size(Q, 1), rows, cols)
+    Kinematics.get_jacobian!(hm, link, joints, with_rot, J, Q; rpy_jac=rpy_jac)
+end
+
+"""Batched IK (damped least squares on the GPU): targets (N, 12) 3x4 poses, Q (N, dof) seeds, solved in place.
+Returns (Q, iters, err); converged where iters < max_iters."""
+function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
+                                        Q::ROCMatrix{T}; max_iters=64, lambda=1e-2, tol_pos=1e-3, tol_rot=1e-3,
+                                        max_step=0.5, with_rot=true, restarts=0, seed=0) where {T}
+    N = size(Q, 1)
+    ids = Int32[j.id for j in joints]
+    p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
+    iters = ROCVector{Int32}(undef, N)
+    err = ROCMatrix{T}(undef, N, 2)
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, with_rot, restarts, seed)
+    check(ccall((:kin_ik_dls_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64,
+                 Ptr{Cvoid}),
+                p, prm, pointer(targets), stride(targets, 2), pointer(Q), stride(Q, 2), N, pointer(iters),
+                pointer(err), N, stream_ptr()))
+    Q, iters, err
+end
+
+function point_inverse_kinematics_nakamura!(hm::HIPModel, link::Link, joints::Vector{<:Joint},
+                                            points::ROCMatrix{T}, Q::ROCMatrix{T}) where {T}
+    N = size(Q, 1)
+    ids = Int32[j.id for j in joints]
+    p = plan!(hm, T, ids, Int32[], Int32(link.id), ids, UInt32(0))
+    check(ccall((:kin_point_ik_nakamura_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{Cvoid}),
+                p, pointer(points), stride(points, 2), pointer(Q), stride(Q, 2), N, stream_ptr()))
+    Q
+end
+
+export HIPModel, point_inverse_kinematics_nakamura!
+
+end # module

@@ -12,6 +12,7 @@
  */
 #include "kin_oracle.h"
 
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -579,6 +580,18 @@ void or_point_ik_nakamura_batch(const or_mech* proto, int64_t n, double* q, int6
 }
 
 /* ---- build-defined DLS IK (see header) ---- */
+static uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double or_ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col) {
+    const uint64_t key = (uint64_t)i * 131ull + (uint64_t)attempt * 31ull + (uint64_t)col + 1ull;
+    return (double)(splitmix64(seed + 0x9E3779B97F4A7C15ull * key) >> 11) * (1.0 / 9007199254740992.0);
+}
+
 /* world-frame rotation vector w with exp([w]) * R = Rt, i.e. log(Rt * R^T) */
 static void rot_error(const tf_t* tgt, const tf_t* now, double w[3]) {
     double E[9]; /* col-major E = Rt * R^T */
@@ -658,6 +671,9 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
             for (int32_t c = 0; c < ndof; ++c) a[c] = q[c * ldq + i];
             int32_t it = 0;
             double ep = 0, er = 0;
+            const int32_t attempt_len = prm->restarts > 0 ? prm->max_iters / (prm->restarts + 1) : 0;
+            double a0[64];
+            for (int32_t c = 0; c < ndof; ++c) a0[c] = a[c];
             for (;; ++it) {
                 or_set_joint_angles(m, n_q, qids, a);
                 tf_t now = get_transform(m, link_id);
@@ -667,6 +683,20 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                 ep = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
                 er = prm->with_rot ? sqrt(e[3] * e[3] + e[4] * e[4] + e[5] * e[5]) : 0.0;
                 if ((ep < prm->tol_pos && er < prm->tol_rot) || it >= prm->max_iters) break;
+                if (attempt_len > 0 && it > 0 && it % attempt_len == 0) {
+                    /* restart: relevant joints re-drawn within limits (U[-pi, pi] if unbounded), base reset */
+                    const int32_t att = it / attempt_len;
+                    for (int32_t c = 0; c < ndof; ++c) {
+                        if (c < n_q && or_is_relevant(m, qids[c], link_id)) {
+                            double l = lo[c], h = hi[c];
+                            if (!isfinite(l) || !isfinite(h)) { l = -3.14159265358979323846; h = 3.14159265358979323846; }
+                            a[c] = l + (h - l) * or_ik_seed_u01(prm->seed, i, att, c);
+                        } else {
+                            a[c] = a0[c];
+                        }
+                    }
+                    continue;
+                }
                 memset(J, 0, sizeof(double) * 6 * ndof);
                 or_get_jacobian(m, link_id, n_q, qids, prm->with_rot, 0, J);
                 double dq[64], mx = 0;

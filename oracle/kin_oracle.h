@@ -108,7 +108,11 @@ typedef struct {
     double tol_rot;    /* |rotation error| (axis-angle) */
     double max_step;   /* clamp on |dq|_inf per iteration */
     int32_t with_rot;
+    int32_t restarts;  /* attempts = restarts + 1, each max_iters / attempts iterations */
+    uint64_t seed;     /* re-seed stream: ik_seed_u01(seed, config index, attempt, column) */
 } or_ik_params;
+/* the restart re-seed draw in [0, 1) shared by the oracle and the GPU kernel */
+double or_ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col);
 void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, int32_t n_q,
                      const int32_t* q_joint_ids, int32_t link_id, const double* target, int64_t ldt,
                      const or_ik_params* prm, int32_t* iters_out, double* err_out, int32_t n_threads);

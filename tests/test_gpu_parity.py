@@ -280,6 +280,24 @@ def test_ik_dls_iterates_vs_oracle(dev, fetch_tree):
         np.testing.assert_array_equal(it.cpu().numpy(), rit)
 
 
+def test_ik_dls_restarts_vs_oracle(dev, fetch_tree):
+    """Restart re-seeding (counter hash of seed, index, attempt, column) identical on both sides."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 300
+    tgt = _targets(om, ids, gl.id, N, 21)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
+    Q = torch.zeros((8, N), dtype=torch.float64, device=dev)
+    Q, it, err = plan.ik_dls(torch.tensor(tgt, device=dev).contiguous(), Q, max_iters=13, restarts=3, seed=77,
+                             tol_pos=1e-12, tol_rot=1e-12)
+    rq, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, max_iters=13, restarts=3, seed=77,
+                                 tol_pos=1e-12, tol_rot=1e-12)
+    np.testing.assert_array_equal(it.cpu().numpy(), rit)
+    np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ik_dls_acceptance(dev, fetch_tree, dtype):
     """Reachable random targets: converged solutions meet the reference test's criteria
