@@ -100,6 +100,60 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
     return out
 
 
+def _coll_leg(ctx, stream, n, steps):
+    """Config 5: FK + SDF validity samples of the planner (src/planning.jl collision check):
+    Fetch arm (8 joints) with 14 build-defined spheres vs the 7-box fridge scene (door at 2.0 rad,
+    base at (1.2, 0, 0)), `n` configurations per GPU, fp32.  Two kernels: min-distance only
+    (the RRT validity test) and per-sphere distances + 14x8 gradients (the planner's constraint).
+    Multi-GPU: each rank samples its own slice; the validity flags are all-gathered over RCCL
+    afterwards (timed separately)."""
+    dt = torch.float32
+    m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    sdf = kinhip.fridge_sdf(fr)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    arm = [m.find_joint(n_) for n_ in ARM]
+    plan = sscc.plan(arm, dtype=dt)
+    Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, start=ctx.rank * n,
+                               seed=555, dtype=dt, device=ctx.device)
+    out = {}
+    for name, kw in (("min_dist", dict(dists=False, min_dist=True)),
+                     ("dists_grads", dict(dists=True, grads=True))):
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                r = plan.run(sdf, Q, stream=stream, **kw)
+        torch.cuda.synchronize()
+        D.barrier(ctx)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            r = plan.run(sdf, Q, stream=stream, **kw)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        D.barrier(ctx)
+        wall, dev_s = D.max_over_ranks(ctx, [time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3])
+        ns = plan.n_sph
+        nbytes = 8 * 4 + (4 if name == "min_dist" else ns * 4 + ns * 8 * 4)
+        out[name] = {"value": n * ctx.world * steps / wall, "unit": "FK+SDF samples/s",
+                     "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
+                     "achieved_GBs": nbytes * n / (dev_s / steps) / 1e9}
+        if name == "min_dist":
+            valid = (r[2] > 0).to(torch.uint8).reshape(1, -1)
+            out[name]["valid_fraction"] = float(valid.float().mean())
+            if ctx.world > 1:
+                torch.cuda.synchronize()
+                D.barrier(ctx)
+                g0 = time.perf_counter()
+                allv = D.all_gather_cols(ctx, valid)
+                torch.cuda.synchronize()
+                out[name]["gather_ms"] = D.max_over_ranks(ctx, [(time.perf_counter() - g0) * 1e3])[0]
+                assert allv.shape[1] == n * ctx.world
+    out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
+                       f"samples sharded across ranks")
+    return out
+
+
 def _cpu_baseline(m, N_budget_s=12.0):
     """Reference-faithful C restatement (oracle/kin_oracle.c) on the host cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -203,6 +257,7 @@ def main():
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9}
         del p2, Q2, P2
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
+        out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = _cpu_baseline(m)
     if rank == 0:

@@ -212,6 +212,40 @@ KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, con
 KINHIP_API int kin_point_ik_nakamura_batch(const kin_plan* p, const void* points, int64_t ldpt, void* q,
                                            int64_t ldq, int64_t n, void* stream);
 
+/* ------------------------------------------------------------------------- */
+/* Collision: swept spheres vs a union of box SDFs                             */
+/* (src/collision.jl:51-103, src/sdf.jl:48-119)           */
+/* ------------------------------------------------------------------------- */
+typedef struct kin_sdf kin_sdf;
+/* UnionSDF of BoxSDF(pose, width) (src/sdf.jl:48-114): box k has world pose
+ * poses16[k] (4x4 column-major) and full widths widths3[k].  Uploaded to the
+ * current device in both precisions. */
+KINHIP_API int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* widths3, kin_sdf** out);
+KINHIP_API int kin_sdf_destroy(kin_sdf* s);
+
+typedef struct kin_coll_desc {
+    int32_t dtype;
+    int32_t n_q;                     /* batch columns (+3 base) and gradient columns */
+    const int32_t* q_joint_ids;
+    int32_t n_spheres;               /* SweptSphereCollisionChecker.sphere_links (src/collision.jl:32-37) */
+    const int32_t* sphere_link_ids;  /* sphere centre = origin of this link ... */
+    const double* centers;           /* ... plus this offset in the link frame ([n][3], NULL = 0) */
+    const double* radii;             /* [n] */
+} kin_coll_desc;
+/* Every sphere must hang (through fixed / non-batched joints) off the chain of
+ * batch joints of one arm (KIN_E_UNSUPPORTED otherwise). */
+KINHIP_API int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* desc, kin_plan** out);
+/* compute_coll_dists(_and_grads)! for N configurations:
+ *   dists    [n_spheres][ldd]       sdf(centre) - radius (or NULL)
+ *   grads    [n_spheres][n_q(+3)][ldg]  grad_sdf^T J(3 x n) of each sphere link (or NULL)
+ *   min_dist [N]                    min over spheres (or NULL)
+ * A sphere farther than `truncation` reports `truncation` and a zero gradient
+ * (truncation_dist, src/collision.jl:84-87).  The SDF gradient is analytic
+ * (the reference takes a forward difference, eps 1e-7). */
+KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq,
+                              int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

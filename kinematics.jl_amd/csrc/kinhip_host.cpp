@@ -159,6 +159,16 @@ struct kin_model {
     }
 };
 
+struct kin_sdf {
+    int32_t n_boxes = 0;
+    void* d_f32 = nullptr;
+    void* d_f64 = nullptr;
+    ~kin_sdf() {
+        if (d_f32) (void)hipFree(d_f32);
+        if (d_f64) (void)hipFree(d_f64);
+    }
+};
+
 struct kin_plan {
     int32_t dtype = KIN_F32;
     int32_t nqcols = 0, rows = 0, ncols = 0, n_q = 0, n_out = 0;
@@ -169,8 +179,13 @@ struct kin_plan {
     KProg<float> pf{};
     KProg<double> pd{};
     LaunchGeom geom{256, 0, 8};
+    // collision plans (kin_coll_plan_create)
+    bool is_coll = false;
+    int32_t n_sph = 0;
+    void* d_sph = nullptr;
     ~kin_plan() {
         if (d_steps) (void)hipFree(d_steps);
+        if (d_sph) (void)hipFree(d_sph);
     }
 };
 
@@ -240,7 +255,15 @@ struct SD {  // staged step, fp64
     bool hasX = false;
     double scale = 1, lo = -INFINITY, hi = INFINITY;
     int32_t kind = MOT_NONE, jkind = MOT_NONE, qcol = -1, flags = 0, out = -1, load = LOAD_NONE, save = -1;
+    int32_t sph0 = 0, sph1 = 0;
     uint64_t colmask = 0;
+};
+
+struct SphD {  // staged collision sphere
+    int32_t step;  // phase-A step whose frame carries it (-1: root frame)
+    double c[3];   // centre in that (canonical) frame
+    double r;
+    int32_t out;
 };
 
 struct Stager {
@@ -254,6 +277,11 @@ struct Stager {
     std::vector<char> hasX;
     std::vector<SD> steps;
     uint64_t zmask = 0;
+    std::vector<int32_t> chain, chain_step;  // phase-A nodes root..spine and their edge steps (-1: none)
+    // collision plans
+    const kin_coll_desc* coll = nullptr;
+    std::vector<SphD> spheres;
+    int32_t sph_root0 = 0, sph_root1 = 0;
     // LDS slots
     std::vector<int> slot_of_link, slot_refs;
     std::vector<int> free_slots;
@@ -359,6 +387,55 @@ struct Stager {
     void emit_subtree_loaded(int32_t v, int slot) {
         emit_subtree(v, slot);
         consume(slot);
+    }
+
+    // spheres = links (src/collision.jl:39-49), each carried by the nearest chain node above it;
+    // the static path from that node (and the node's canonical-frame correction) is folded into
+    // the centre, in fp64
+    int stage_spheres(int32_t sroot) {
+        const int32_t L = m.n_links;
+        std::vector<int32_t> on_chain(L, -1);
+        for (size_t k = 0; k < chain.size(); ++k) on_chain[chain[k]] = (int32_t)k;
+        for (int32_t k = 0; k < coll->n_spheres; ++k) {
+            const int32_t lk = coll->sphere_link_ids[k] - 1;
+            if (lk < 0 || lk >= L) return set_error(KIN_E_KEY, "coll plan: sphere link id out of range");
+            std::vector<int32_t> path;
+            int32_t x = lk;
+            while (x >= 0 && on_chain[x] < 0) {
+                const int32_t j = m.link_pjoint[x];
+                if (j < 0) break;
+                if (moving[j])
+                    return set_error(KIN_E_UNSUPPORTED, "coll plan: sphere " + std::to_string(k) +
+                                                            " hangs off a moving joint outside the chain");
+                path.push_back(j);
+                x = m.plink(x);
+            }
+            if (x < 0 || on_chain[x] < 0)
+                return set_error(KIN_E_UNSUPPORTED, "coll plan: sphere " + std::to_string(k) + " is on another tree");
+            M34 S = hasX[x] ? Xinv[x] : m_identity();
+            for (size_t pi = path.size(); pi-- > 0;) S = m_mul(S, m.joint_tf(path[pi], m.angles[path[pi]]));
+            SphD sd;
+            const double c0 = coll->centers ? coll->centers[3 * k] : 0.0;
+            const double c1 = coll->centers ? coll->centers[3 * k + 1] : 0.0;
+            const double c2 = coll->centers ? coll->centers[3 * k + 2] : 0.0;
+            for (int i = 0; i < 3; ++i) sd.c[i] = S.r[3 * i] * c0 + S.r[3 * i + 1] * c1 + S.r[3 * i + 2] * c2 + S.t[i];
+            sd.r = coll->radii[k];
+            sd.out = k;
+            sd.step = (x == sroot) ? -1 : chain_step[on_chain[x]];
+            if (x != sroot && sd.step < 0) return set_error(KIN_E_INVALID, "coll plan: internal (no step)");
+            spheres.push_back(sd);
+        }
+        std::stable_sort(spheres.begin(), spheres.end(), [](const SphD& a, const SphD& b) { return a.step < b.step; });
+        for (size_t k = 0; k < spheres.size(); ++k) {
+            const int32_t st = spheres[k].step;
+            if (st < 0) {
+                sph_root1 = (int32_t)k + 1;
+            } else {
+                if (steps[st].sph1 == 0) steps[st].sph0 = (int32_t)k;
+                steps[st].sph1 = (int32_t)k + 1;
+            }
+        }
+        return KIN_OK;
     }
 
     int run(kin_plan& P) {
@@ -468,7 +545,7 @@ struct Stager {
         int32_t lhx = 0;
         slot_of_link.assign(L, -1);
         if (spine >= 0) {
-            std::vector<int32_t> chain;  // nodes root..spine
+            chain.clear();  // nodes root..spine
             for (int32_t x = spine; x >= 0; x = cparent(x)) chain.push_back(x);
             std::reverse(chain.begin(), chain.end());
             sroot = chain[0];
@@ -502,6 +579,7 @@ struct Stager {
                 Xl = Xinv[spine];
                 lhx = hasX[spine];
             }
+            chain_step = edge_step;
             nA = (int32_t)steps.size();
             if (nA > kMaxChain)
                 return set_error(KIN_E_UNSUPPORTED, "plan: root -> spine chain has " + std::to_string(nA) +
@@ -528,6 +606,10 @@ struct Stager {
                 steps.push_back(pad);
             }
             nA = bound;
+        }
+        if (coll) {
+            const int rc = stage_spheres(sroot);
+            if (rc != KIN_OK) return rc;
         }
         // ---- phase B ----
         for (auto& pc : pending) {
@@ -582,6 +664,9 @@ struct Stager {
             K.last_has_x = lhx;
             K.spine_out = spine_out;
             K.zmask = zmask;
+            K.n_sph = (int32_t)spheres.size();
+            K.sph_root0 = sph_root0;
+            K.sph_root1 = sph_root1;
             to_row12<T>(Xl, K.Xlast);
             for (size_t s = 0; s < steps.size(); ++s) {
                 const SD& a = steps[s];
@@ -599,6 +684,8 @@ struct Stager {
                 b.out = a.out;
                 b.load = a.load;
                 b.save = a.save;
+                b.sph0 = a.sph0;
+                b.sph1 = a.sph1;
                 b.colmask = a.colmask;
             }
         };
@@ -620,6 +707,31 @@ struct Stager {
         }
         e = hipMemcpy(P.d_steps, host.data(), bytes, hipMemcpyHostToDevice);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+        if (coll) {
+            P.is_coll = true;
+            P.n_sph = (int32_t)spheres.size();
+            auto put = [&](auto* tag) -> int {
+                using TS = std::remove_pointer_t<decltype(tag)>;
+                std::vector<TS> hs(std::max<size_t>(1, spheres.size()));
+                memset(hs.data(), 0, sizeof(TS) * hs.size());
+                for (size_t k = 0; k < spheres.size(); ++k) {
+                    for (int i = 0; i < 3; ++i) hs[k].c[i] = spheres[k].c[i];
+                    hs[k].r = spheres[k].r;
+                    hs[k].out = spheres[k].out;
+                }
+                const size_t nb = sizeof(TS) * hs.size();
+                hipError_t e2 = hipMalloc(&P.d_sph, nb);
+                if (e2 != hipSuccess) {
+                    P.d_sph = nullptr;
+                    return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e2));
+                }
+                e2 = hipMemcpy(P.d_sph, hs.data(), nb, hipMemcpyHostToDevice);
+                if (e2 != hipSuccess) return set_error(KIN_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e2));
+                return KIN_OK;
+            };
+            const int rc = d.dtype == KIN_F32 ? put((KSphere<float>*)nullptr) : put((KSphere<double>*)nullptr);
+            if (rc != KIN_OK) return rc;
+        }
 
         // IK eligibility: Jacobian joints == q joints (same order, no repeats), no rpy rows
         P.ik_ok = has_jac && d.n_jac == d.n_q && !(d.jac_flags & KIN_RPY_JAC);
@@ -837,6 +949,95 @@ int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_id, int32_t
     const int rc = cached_plan(m, d, &p);
     if (rc != KIN_OK) return rc;
     return kin_plan_run(p, q, ldq, n, pose, ldp, jac, ldj, stream);
+}
+
+int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* widths3, kin_sdf** out) {
+    if (!out || n_boxes < 1 || !poses16 || !widths3)
+        return set_error(KIN_E_INVALID, "kin_sdf_create_boxes: need >= 1 box and non-null arrays");
+    auto sd = std::make_unique<kin_sdf>();
+    sd->n_boxes = n_boxes;
+    std::vector<KBox<float>> bf(n_boxes);
+    std::vector<KBox<double>> bd(n_boxes);
+    for (int32_t k = 0; k < n_boxes; ++k) {
+        const M34 inv = m_rigid_inverse(m_from_col16(poses16 + 16 * k));  // BoxSDF.inv_pose (src/sdf.jl:60)
+        to_row12<float>(inv, bf[k].inv);
+        to_row12<double>(inv, bd[k].inv);
+        for (int i = 0; i < 3; ++i) {
+            bf[k].half[i] = (float)(0.5 * widths3[3 * k + i]);
+            bd[k].half[i] = 0.5 * widths3[3 * k + i];
+        }
+        bf[k].pad = 0;
+        bd[k].pad = 0;
+    }
+    hipError_t e = hipMalloc(&sd->d_f32, sizeof(KBox<float>) * n_boxes);
+    if (e == hipSuccess) e = hipMalloc(&sd->d_f64, sizeof(KBox<double>) * n_boxes);
+    if (e == hipSuccess) e = hipMemcpy(sd->d_f32, bf.data(), sizeof(KBox<float>) * n_boxes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sd->d_f64, bd.data(), sizeof(KBox<double>) * n_boxes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("kin_sdf_create_boxes: ") + hipGetErrorString(e));
+    *out = sd.release();
+    return KIN_OK;
+}
+
+int kin_sdf_destroy(kin_sdf* s) {
+    delete s;
+    return KIN_OK;
+}
+
+int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** out) {
+    if (!m || !c || !out) return set_error(KIN_E_INVALID, "kin_coll_plan_create: null argument");
+    if (c->n_spheres < 1 || !c->sphere_link_ids || !c->radii)
+        return set_error(KIN_E_INVALID, "kin_coll_plan_create: need >= 1 sphere with link ids and radii");
+    if (c->n_q < 0 || (c->n_q && !c->q_joint_ids)) return set_error(KIN_E_INVALID, "kin_coll_plan_create: bad q");
+    const int32_t L = m->n_links, J = m->n_joints();
+    std::vector<char> moving(J, 0);
+    for (int32_t k = 0; k < c->n_q; ++k) {
+        const int32_t j = c->q_joint_ids[k] - 1;
+        if (j < 0 || j >= J) return set_error(KIN_E_KEY, "kin_coll_plan_create: q joint id out of range");
+        moving[j] = m->jtype[j] != KIN_JOINT_FIXED;
+    }
+    // spine: the sphere anchor (nearest link below a moving joint) with the most moving joints above it
+    int32_t spine = -1, best = -1;
+    for (int32_t k = 0; k < c->n_spheres; ++k) {
+        int32_t x = c->sphere_link_ids[k] - 1;
+        if (x < 0 || x >= L) return set_error(KIN_E_KEY, "kin_coll_plan_create: sphere link id out of range");
+        while (x >= 0 && m->link_pjoint[x] >= 0 && !moving[m->link_pjoint[x]]) x = m->plink(x);
+        int depth = 0;
+        for (int32_t y = x; y >= 0 && m->link_pjoint[y] >= 0; y = m->plink(y)) depth += moving[m->link_pjoint[y]];
+        if (depth > best) {
+            best = depth;
+            spine = x;
+        }
+    }
+    kin_plan_desc d{c->dtype, c->n_q, c->q_joint_ids, 0, nullptr, spine + 1, c->n_q, c->q_joint_ids, 0};
+    auto P = std::make_unique<kin_plan>();
+    Stager st(*m, d);
+    st.coll = c;
+    const int rc = st.run(*P);
+    if (rc != KIN_OK) return rc;
+    *out = P.release();
+    return KIN_OK;
+}
+
+int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq, int64_t n,
+                   void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream) {
+    if (!p || !sdf) return set_error(KIN_E_INVALID, "kin_coll_batch: null plan / sdf");
+    if (!p->is_coll) return set_error(KIN_E_INVALID, "kin_coll_batch: plan was not made by kin_coll_plan_create");
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if ((p->nqcols > 0 && (!q || ldq < n)) || (dists && ldd < n) || (grads && ldg < n))
+        return set_error(KIN_E_INVALID, "kin_coll_batch: bad pointer / stride");
+    CollArgs a{truncation, sdf->n_boxes};
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
+                               (const KBox<float>*)sdf->d_f32, p->geom, a, (const float*)q, ldq, n, (float*)dists, ldd,
+                               (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
+    else
+        e = launch_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
+                                (const KBox<double>*)sdf->d_f64, p->geom, a, (const double*)q, ldq, n, (double*)dists,
+                                ldd, (double*)grads, ldg, (double*)min_dist, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
+    return KIN_OK;
 }
 
 int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, void* q,

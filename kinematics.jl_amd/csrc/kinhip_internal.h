@@ -36,4 +36,14 @@ template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
                            int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st);
 
+struct CollArgs {
+    double truncation;
+    int32_t n_boxes;
+};
+
+template <typename T>
+hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                       const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
+                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st);
+
 }  // namespace kinhip

@@ -45,8 +45,29 @@ struct KStep {
     int32_t out;    // output index (-1: none)
     int32_t load;   // LOAD_NONE: continue, LOAD_ROOT: root frame, >=0: LDS slot
     int32_t save;   // LDS slot to save C into (-1: none)
+    int32_t sph0;   // collision plans: spheres [sph0, sph1) hang off this step's frame
+    int32_t sph1;
     int32_t pad1;
     uint64_t colmask;  // Jacobian columns this record feeds (phase A only)
+};
+
+// collision sphere (src/collision.jl:39-49): centre in the canonical frame of
+// its phase-A step (or the root frame), radius, output index
+template <typename T>
+struct KSphere {
+    T c[3];
+    T r;
+    int32_t out;  // output row (the caller's sphere order)
+    int32_t pad[3];
+};
+
+// one BoxSDF of a UnionSDF (src/sdf.jl:48-114): inverse world pose (row-major
+// 3x4) and half widths
+template <typename T>
+struct KBox {
+    T inv[12];
+    T half[3];
+    T pad;
 };
 
 template <typename T>
@@ -61,6 +82,9 @@ struct KProg {
     int32_t last_has_x;
     int32_t spine_out;  // output index of the spine link written after phase A (-1: none)
     int32_t pad;
+    int32_t n_sph;      // collision plans
+    int32_t sph_root0, sph_root1;  // spheres on the root frame
+    int32_t pad2;
     uint64_t zmask;    // irrelevant Jacobian columns (zero-filled with PF_ZERO)
     T Xlast[12];       // spine link frame = C(after phase A) * Xlast
 };

@@ -13,6 +13,10 @@ from .mechanism import (  # noqa: F401
     parent_link, parse_urdf, point_inverse_kinematics_nakamura, rpy, set_joint_angles,
 )
 from .synth import uniform_configs  # noqa: F401
+from .collision import (  # noqa: F401
+    FETCH_ARM_SPHERES, BoxSDF, CollisionPlan, SweptSphereCollisionChecker, UnionSDF, add_fetch_arm_spheres,
+    compute_coll_dists, compute_coll_dists_and_grads, fridge_sdf,
+)
 
 FETCH_ARM_JOINTS = [
     "torso_lift_joint", "shoulder_pan_joint", "shoulder_lift_joint", "upperarm_roll_joint",

@@ -34,6 +34,7 @@ EXPORTS = [
     "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
+    "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
 ]
 
 
@@ -56,6 +57,12 @@ class PlanDesc(C.Structure):
                 ("n_out", C.c_int32), ("out_link_ids", C.c_void_p),
                 ("jac_link_id", C.c_int32), ("n_jac", C.c_int32), ("jac_joint_ids", C.c_void_p),
                 ("jac_flags", C.c_uint32)]
+
+
+class CollDesc(C.Structure):
+    _fields_ = [("dtype", C.c_int32), ("n_q", C.c_int32), ("q_joint_ids", C.c_void_p),
+                ("n_spheres", C.c_int32), ("sphere_link_ids", C.c_void_p), ("centers", C.c_void_p),
+                ("radii", C.c_void_p)]
 
 
 class IkParams(C.Structure):
@@ -104,6 +111,10 @@ def lib():
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),
         "kin_ik_dls_batch": ([P, P, P, I64, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_point_ik_nakamura_batch": ([P, P, I64, P, I64, I64, P], C.c_int),
+        "kin_sdf_create_boxes": ([I32, P, P, P], C.c_int),
+        "kin_sdf_destroy": ([P], C.c_int),
+        "kin_coll_plan_create": ([P, P, P], C.c_int),
+        "kin_coll_batch": ([P, P, C.c_double, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -1,0 +1,178 @@
+"""Swept-sphere collision against box SDFs (src/sdf.jl, src/collision.jl) on the GPU.
+
+Mirrors the reference names: ``BoxSDF(pose, width)``, ``UnionSDF(sdfs)`` /
+``UnionSDF(mechanism)`` (one box per link with box collision geometry,
+src/sdf.jl:82-97), ``SweptSphereCollisionChecker(mech)``,
+``compute_coll_dists`` / ``compute_coll_dists_and_grads`` (single
+configuration) and the batched ``CollisionPlan``.  Spheres are links added
+with ``add_new_link`` exactly as ``add_coll_links`` does
+(src/collision.jl:39-49); the sphere geometry itself comes from the caller
+(``add_coll_sphere``): the reference derives it from mesh files with
+skrobot + trimesh, which are not available here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import itertools
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as K
+from .mechanism import Link, Mechanism, _device, _i32, _p, get_transform
+
+_DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
+_uid = itertools.count()
+
+
+class BoxSDF:
+    """src/sdf.jl:48-74: a box of full widths `width` at world pose `pose` (4x4)."""
+
+    def __init__(self, pose, width):
+        self.pose = np.asarray(pose, np.float64).reshape(4, 4)
+        self.width = np.asarray(width, np.float64).reshape(3)
+
+    def __call__(self, p):  # host convenience (the GPU path is kin_coll_batch)
+        R, t = self.pose[:3, :3], self.pose[:3, 3]
+        q = np.abs(R.T @ (np.asarray(p, np.float64) - t)) - 0.5 * self.width
+        return float(np.linalg.norm(np.maximum(q, 0.0)) + min(q.max(), 0.0))
+
+
+class UnionSDF:
+    """src/sdf.jl:76-119: min over boxes.  ``UnionSDF(mech)`` uses the mechanism's current angles."""
+
+    def __init__(self, sdfs_or_mech):
+        if isinstance(sdfs_or_mech, Mechanism):
+            m = sdfs_or_mech
+            boxes = []
+            for l in m.links:
+                meta = l.geometric_meta_data
+                if meta is not None and hasattr(meta, "extents"):
+                    boxes.append(BoxSDF(get_transform(m, l) @ meta.origin, meta.extents))
+            sdfs = boxes
+        else:
+            sdfs = list(sdfs_or_mech)
+        if not sdfs:
+            raise ValueError("UnionSDF needs at least one box")
+        self.sdfs = sdfs
+        P = np.ascontiguousarray(np.array([b.pose.T.reshape(16) for b in sdfs], np.float64).reshape(-1))
+        W = np.ascontiguousarray(np.array([b.width for b in sdfs], np.float64).reshape(-1))
+        self._h = C.c_void_p()
+        K.check(K.lib().kin_sdf_create_boxes(len(sdfs), _p(P), _p(W), C.byref(self._h)))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and K._lib is not None:
+            K._lib.kin_sdf_destroy(self._h)
+            self._h = None
+
+    def __call__(self, p):
+        return min(b(p) for b in self.sdfs)
+
+
+class SweptSphereCollisionChecker:
+    """src/collision.jl:32-49: spheres are fixed child links of the mechanism's links."""
+
+    def __init__(self, mech: Mechanism):
+        self.mech = mech
+        self.sphere_links: list = []
+        self.sphere_radii: list = []
+
+    def add_coll_sphere(self, link: Link, center, radius: float) -> Link:
+        sl = Link(f"sphere_{next(_uid)}", link_type="CollSphere")
+        self.mech.add_new_link(sl, link, np.asarray(center, np.float64))
+        self.sphere_links.append(sl)
+        self.sphere_radii.append(float(radius))
+        return sl
+
+    def plan(self, joints, dtype=torch.float32) -> "CollisionPlan":
+        return CollisionPlan(self, joints, dtype)
+
+
+class CollisionPlan:
+    def __init__(self, sscc: SweptSphereCollisionChecker, joints, dtype):
+        m = sscc.mech
+        m._sync_angles()
+        self.dtype = dtype
+        self.n_sph = len(sscc.sphere_links)
+        self.n_dof = len(joints) + (3 if m.with_base else 0)
+        self._q = _i32([j.id for j in joints])
+        self._s = _i32([l.id for l in sscc.sphere_links])
+        self._r = np.ascontiguousarray(np.asarray(sscc.sphere_radii, np.float64))
+        d = K.CollDesc(_DT[dtype], self._q.size, _p(self._q).value, self._s.size, _p(self._s).value, None,
+                       _p(self._r).value)
+        self._h = C.c_void_p()
+        K.check(K.lib().kin_coll_plan_create(m._model, C.byref(d), C.byref(self._h)))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and K._lib is not None:
+            K._lib.kin_plan_destroy(self._h)
+            self._h = None
+
+    def run(self, sdf: UnionSDF, Q: torch.Tensor, dists=True, grads=False, min_dist=False,
+            truncation=float("inf"), stream=None):
+        """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async."""
+        if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
+            raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
+        N = Q.shape[1]
+        dev = Q.device
+        D = torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None
+        G = torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None
+        Mn = torch.empty(N, dtype=self.dtype, device=dev) if min_dist else None
+        st = (stream or torch.cuda.current_stream(dev)).cuda_stream
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        K.check(K.lib().kin_coll_batch(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0), N, ptr(D), N,
+                                       ptr(G), N, ptr(Mn), st))
+        return D, G, Mn
+
+
+def compute_coll_dists(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF) -> np.ndarray:
+    """src/collision.jl:60-65 at the mechanism's current angles (GPU, batch of one)."""
+    d, _ = compute_coll_dists_and_grads(sscc, joints, sdf, with_grad=False)
+    return d
+
+
+def compute_coll_dists_and_grads(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF,
+                                 truncation_dist=float("inf"), with_grad=True):
+    """src/collision.jl:96-103: (vals [n_sph], grads [n_dof, n_sph])."""
+    dev = _device()
+    m = sscc.mech
+    plan = CollisionPlan(sscc, joints, torch.float64)
+    Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    D, G, _ = plan.run(sdf, Q, dists=True, grads=with_grad, truncation=truncation_dist)
+    vals = D[:, 0].cpu().numpy()
+    return vals, (G[:, :, 0].cpu().numpy().T if with_grad else None)
+
+
+# Build-defined sphere approximation of the Fetch arm (the reference computes
+# spheres from collision meshes with skrobot/trimesh: unavailable offline).
+# (link, centre in the link frame, radius); the arm links extend along +x.
+FETCH_ARM_SPHERES = [
+    ("shoulder_pan_link", (0.06, 0.0, 0.06), 0.08),
+    ("shoulder_lift_link", (0.05, 0.0, 0.0), 0.07),
+    ("shoulder_lift_link", (0.15, 0.0, 0.0), 0.07),
+    ("upperarm_roll_link", (0.05, 0.0, 0.0), 0.065),
+    ("upperarm_roll_link", (0.12, 0.0, 0.0), 0.065),
+    ("elbow_flex_link", (0.05, 0.0, 0.0), 0.06),
+    ("elbow_flex_link", (0.13, 0.0, 0.0), 0.06),
+    ("forearm_roll_link", (0.05, 0.0, 0.0), 0.055),
+    ("forearm_roll_link", (0.12, 0.0, 0.0), 0.055),
+    ("wrist_flex_link", (0.05, 0.0, 0.0), 0.05),
+    ("wrist_flex_link", (0.10, 0.0, 0.0), 0.05),
+    ("wrist_roll_link", (0.06, 0.0, 0.0), 0.05),
+    ("gripper_link", (-0.05, 0.0, 0.0), 0.05),
+    ("gripper_link", (0.0, 0.0, 0.0), 0.045),
+]
+
+
+def add_fetch_arm_spheres(sscc: SweptSphereCollisionChecker):
+    for name, c, r in FETCH_ARM_SPHERES:
+        sscc.add_coll_sphere(sscc.mech.find_link(name), c, r)
+    return sscc
+
+
+def fridge_sdf(fridge: Mechanism, door_angle=2.0, base=(1.2, 0.0, 0.0)) -> UnionSDF:
+    """The fridge scene of test/test_inverse_kinematics.jl:52-70 (door at 2.0 rad, base (1.2, 0, 0))."""
+    door = fridge.find_joint("door_joint")
+    fridge.set_joint_angles([door], [door_angle, *base])
+    return UnionSDF(fridge)

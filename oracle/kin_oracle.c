@@ -740,3 +740,110 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
         or_mech_destroy(m);
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* SDF + swept-sphere collision (src/sdf.jl, src/collision.jl)          */
+/* ------------------------------------------------------------------ */
+static tf_t tf_inv(const tf_t* t) { /* src/transform.jl:62-65 */
+    tf_t r = tf_identity();
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) M(r, i, j) = M(*t, j, i);
+    for (int i = 0; i < 3; ++i)
+        M(r, i, 3) = -(M(r, i, 0) * M(*t, 0, 3) + M(r, i, 1) * M(*t, 1, 3) + M(r, i, 2) * M(*t, 2, 3));
+    return r;
+}
+
+or_union_sdf* or_sdf_create(int32_t n, const double* poses16, const double* widths3) {
+    or_union_sdf* s = (or_union_sdf*)calloc(1, sizeof(or_union_sdf));
+    s->n_boxes = n;
+    s->inv_pose = (double*)malloc(sizeof(double) * 16 * (n + 1));
+    s->width = (double*)malloc(sizeof(double) * 3 * (n + 1));
+    for (int32_t k = 0; k < n; ++k) {
+        tf_t t; memcpy(t.m, poses16 + 16 * k, sizeof t.m);
+        tf_t r = tf_inv(&t);
+        memcpy(s->inv_pose + 16 * k, r.m, sizeof r.m);
+        memcpy(s->width + 3 * k, widths3 + 3 * k, sizeof(double) * 3);
+    }
+    return s;
+}
+
+void or_sdf_destroy(or_union_sdf* s) {
+    if (!s) return;
+    free(s->inv_pose); free(s->width); free(s);
+}
+
+double or_box_sdf(const or_union_sdf* s, int32_t k, const double* p) {
+    const double* T = s->inv_pose + 16 * k;
+    double q[3], mx = -INFINITY, nrm = 0;
+    for (int i = 0; i < 3; ++i) {
+        /* inv_pose * p = translation + rotation * p (src/transform.jl:39-41) */
+        double l = T[12 + i] + (T[i] * p[0] + T[4 + i] * p[1] + T[8 + i] * p[2]);
+        q[i] = fabs(l) - 0.5 * s->width[3 * k + i];
+        if (q[i] > mx) mx = q[i];
+        double c = q[i] > 0 ? q[i] : 0.0;
+        nrm += c * c;
+    }
+    return sqrt(nrm) + (mx < 0 ? mx : 0.0);
+}
+
+double or_union_sdf_value(const or_union_sdf* s, const double* p, int32_t* argmin) {
+    double best = INFINITY;
+    int32_t bi = 0;
+    for (int32_t k = 0; k < s->n_boxes; ++k) {
+        double v = or_box_sdf(s, k, p);
+        if (v < best) { best = v; bi = k; }  /* argmin: first minimum */
+    }
+    if (argmin) *argmin = bi;
+    return best;
+}
+
+void or_union_sdf_gradient(const or_union_sdf* s, const double* p, double* g) {
+    int32_t k;
+    double v0 = or_union_sdf_value(s, p, &k);
+    const double eps = 1e-7;
+    for (int i = 0; i < 3; ++i) {
+        double t[3] = {p[0], p[1], p[2]};
+        t[i] += eps;
+        g[i] = (or_box_sdf(s, k, t) - v0) / eps;
+    }
+}
+
+void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, const double* q, int64_t ldq,
+                   int32_t n_q, const int32_t* qids, int32_t n_sph, const int32_t* sph, const double* radii,
+                   double trunc, double* dists, int64_t ldd, double* grads, int64_t ldg, int32_t n_threads) {
+    int nt = nthreads_of(n_threads);
+    int32_t ncolq = n_q + (proto->with_base ? 3 : 0);
+#pragma omp parallel num_threads(nt)
+    {
+        or_mech* m = or_mech_clone(proto);
+        double* a = (double*)malloc(sizeof(double) * (ncolq + 1));
+        double* J = (double*)malloc(sizeof(double) * 3 * (ncolq + 1));
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < n; ++i) {
+            for (int32_t c = 0; c < ncolq; ++c) a[c] = q[c * ldq + i];
+            or_set_joint_angles(m, n_q, qids, a);
+            for (int32_t k = 0; k < n_sph; ++k) {
+                tf_t t = get_transform(m, sph[k]);
+                double p[3] = {M(t, 0, 3), M(t, 1, 3), M(t, 2, 3)};
+                double d0 = or_union_sdf_value(sdf, p, NULL) - radii[k];
+                if (d0 > trunc) {
+                    dists[(size_t)k * ldd + i] = trunc;
+                    if (grads)
+                        for (int32_t c = 0; c < ncolq; ++c) grads[((size_t)k * ncolq + c) * ldg + i] = 0.0;
+                    continue;
+                }
+                dists[(size_t)k * ldd + i] = d0;
+                if (grads) {
+                    double g[3];
+                    or_union_sdf_gradient(sdf, p, g);
+                    memset(J, 0, sizeof(double) * 3 * ncolq);
+                    or_get_jacobian(m, sph[k], n_q, qids, 0, 0, J);
+                    for (int32_t c = 0; c < ncolq; ++c)
+                        grads[((size_t)k * ncolq + c) * ldg + i] = g[0] * J[3 * c] + g[1] * J[3 * c + 1] + g[2] * J[3 * c + 2];
+                }
+            }
+        }
+        free(a); free(J);
+        or_mech_destroy(m);
+    }
+}

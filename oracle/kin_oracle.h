@@ -117,6 +117,31 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                      const int32_t* q_joint_ids, int32_t link_id, const double* target, int64_t ldt,
                      const or_ik_params* prm, int32_t* iters_out, double* err_out, int32_t n_threads);
 
+/* ---- signed distance fields and swept-sphere collision (src/sdf.jl, src/collision.jl) ----
+ * Boxes: world pose (4x4 column-major) + full widths; the union is the min over
+ * boxes (src/sdf.jl:108-114, argmin = first minimum). */
+typedef struct {
+    int32_t n_boxes;
+    double* inv_pose;  /* [n][16] column-major inverse world poses (BoxSDF.inv_pose) */
+    double* width;     /* [n][3] */
+} or_union_sdf;
+or_union_sdf* or_sdf_create(int32_t n_boxes, const double* poses16, const double* widths3);
+void or_sdf_destroy(or_union_sdf* s);
+/* BoxSDF value (src/sdf.jl:67-74) of box k at world point p */
+double or_box_sdf(const or_union_sdf* s, int32_t k, const double* p);
+/* UnionSDF value (src/sdf.jl:108-114); *argmin (0-based) may be NULL */
+double or_union_sdf_value(const or_union_sdf* s, const double* p, int32_t* argmin);
+/* gradient! of the union (src/sdf.jl:34-41, 116-119): forward difference, eps 1e-7, on the min box */
+void or_union_sdf_gradient(const or_union_sdf* s, const double* p, double* grad3);
+/* compute_coll_dists_and_grads! (src/collision.jl:67-94) for a batch: sphere k is link sph_links[k]
+ * (its origin is the sphere centre, src/collision.jl:39-49) with radius radii[k].
+ * dists: [n_sph][ldd]; grads (nullable): [n_sph][n_dof][ldg] with n_dof = n_q (+3 base);
+ * dist > truncation -> value = truncation, gradient 0. */
+void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, const double* q, int64_t ldq,
+                   int32_t n_q, const int32_t* q_joint_ids, int32_t n_sph, const int32_t* sph_links,
+                   const double* radii, double truncation, double* dists, int64_t ldd, double* grads,
+                   int64_t ldg, int32_t n_threads);
+
 #ifdef __cplusplus
 }
 #endif

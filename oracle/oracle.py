@@ -187,6 +187,15 @@ def lib():
         L.or_fk_jac_batch.argtypes = [P, I64, P, I64, I32, P, I32, I32, P, I32, I32, I32, P, I64, P, I64, I32]
         L.or_point_ik_nakamura_batch.argtypes = [P, I64, P, I64, I32, P, I32, P, I64, I32]
         L.or_ik_dls_batch.argtypes = [P, I64, P, I64, I32, P, I32, P, I64, P, P, P, I32]
+        L.or_sdf_create.restype = P
+        L.or_sdf_create.argtypes = [I32, P, P]
+        L.or_sdf_destroy.argtypes = [P]
+        L.or_box_sdf.restype = D
+        L.or_box_sdf.argtypes = [P, I32, P]
+        L.or_union_sdf_value.restype = D
+        L.or_union_sdf_value.argtypes = [P, P, P]
+        L.or_union_sdf_gradient.argtypes = [P, P, P]
+        L.or_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, P, D, P, I64, P, I64, I32]
         _lib = L
     return _lib
 
@@ -335,3 +344,60 @@ def rpy(T):
     out = np.zeros(3)
     lib().or_rpy(_p(tf_colmajor(T)), _p(out))
     return out
+
+
+class OracleUnionSDF:
+    """UnionSDF of BoxSDFs (src/sdf.jl:48-114): boxes given by world pose (4x4) and full widths."""
+
+    def __init__(self, poses, widths):
+        poses = np.asarray(poses, np.float64).reshape(-1, 4, 4)
+        self.n = poses.shape[0]
+        P = _f64(np.transpose(poses, (0, 2, 1)).reshape(-1))
+        W = _f64(np.asarray(widths, np.float64).reshape(-1))
+        self._h = lib().or_sdf_create(self.n, _p(P), _p(W))
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.or_sdf_destroy(self._h)
+            self._h = None
+
+    def box(self, k, p):
+        return lib().or_box_sdf(self._h, int(k), _p(_f64(p)))
+
+    def __call__(self, p):
+        return lib().or_union_sdf_value(self._h, _p(_f64(p)), None)
+
+    def gradient(self, p):
+        g = np.zeros(3)
+        lib().or_union_sdf_gradient(self._h, _p(_f64(p)), _p(g))
+        return g
+
+
+def coll_batch(mech: "OracleMech", sdf: OracleUnionSDF, q, q_joint_ids, sphere_links, radii, truncation=np.inf,
+               with_grad=True, n_threads=0):
+    """-> dists [n_sph, N], grads [n_sph, n_dof, N] (compute_coll_dists_and_grads!, src/collision.jl:67-94)."""
+    q = _f64(q)
+    ids = _i32(q_joint_ids)
+    sph = _i32(sphere_links)
+    r = _f64(radii)
+    N = q.shape[1]
+    ndof = ids.size + (3 if mech.with_base else 0)
+    d = np.zeros((sph.size, N))
+    g = np.zeros((sph.size, ndof, N)) if with_grad else None
+    lib().or_coll_batch(mech._h, sdf._h, N, _p(q), N, ids.size, _p(ids), sph.size, _p(sph), _p(r),
+                        float(truncation), _p(d), N, _p(g) if with_grad else None, N, n_threads)
+    return d, g
+
+
+def fridge_boxes(tree: UrdfTree, door_angle=2.0, base=(1.2, 0.0, 0.0)):
+    """UnionSDF(fridge) of test/test_inverse_kinematics.jl:52-70: one BoxSDF per URDF link with a box
+    collision, attached at the collision origin (src/sdf.jl:82-97), world poses with the fridge's
+    planar base and door joint set."""
+    m = OracleMech(tree, with_base=True)
+    door = tree.joint_id("door_joint")
+    m.set_joint_angles([door], [door_angle, *base])
+    poses, widths = [], []
+    for lid, (ext, org) in sorted(tree.link_box.items()):
+        poses.append(m.get_transform(lid) @ org)
+        widths.append(ext)
+    return np.array(poses), np.array(widths)

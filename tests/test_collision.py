@@ -1,0 +1,163 @@
+"""SDF + swept-sphere collision (config 5 of BASELINE.json).
+
+CPU (oracle, pinned by the reference's tests):
+  test/test_sdf.jl:16-36   BoxSDF / UnionSDF known answers
+  test/test_sdf.jl:38-54   fridge UnionSDF gradient vs finite differences (seeded points)
+  test/test_collision.jl   analytic (grad_sdf^T J) vs finite-difference collision gradient, atol 1e-5
+GPU: k_coll vs the oracle (distances: fp64 1e-9 / fp32 2e-5; gradients vs the oracle's
+forward-difference gradient: 2e-5 in fp64) and vs finite differences of its own distances.
+Sphere geometry is build-defined (kinhip.FETCH_ARM_SPHERES): the reference derives it from mesh
+files that are not available offline, so sphere placement itself is parity-unpinned.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import ARM, golden
+
+
+def _T(t=(0, 0, 0), R=None):
+    T = np.eye(4)
+    if R is not None:
+        T[:3, :3] = R
+    T[:3, 3] = t
+    return T
+
+
+def _rotz(a):
+    return np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+
+
+def test_box_sdf_known_answers():
+    pose = _T((0.5, 0.5, 0.5), _rotz(0.3))
+    s = O.OracleUnionSDF([pose], [[1, 1, 1]])
+    at = lambda v: (pose @ np.r_[v, 1.0])[:3]
+    assert abs(s(at([0.5, 0.5, 0.5]))) < 1e-12
+    assert abs(s(at([0, 0, 0])) + 0.5) < 1e-12
+    assert abs(s(at([0, 0, 1])) - 0.5) < 1e-12
+
+
+def test_union_sdf_known_answers():
+    p1, p2 = _T((0.5, 0.5, 0.0)), _T((-0.5, -0.5, 0.0))
+    u = O.OracleUnionSDF([p1, p2], [[1, 1, 1], [1, 1, 1]])
+    at = lambda P, v: (P @ np.r_[v, 1.0])[:3]
+    assert abs(u(at(p1, [0.5, 0.5, 0.5]))) < 1e-12
+    assert abs(u(at(p2, [-0.5, -0.5, -0.5]))) < 1e-12
+    assert abs(u(at(p1, [0.5, 0.5, 1.5])) - 1.0) < 1e-12
+    assert abs(u(at(p1, [-0.5, -0.5, -1.5])) - 1.0) < 1e-12
+
+
+def test_fridge_union_gradient():
+    """test/test_sdf.jl:38-54 with a seeded point cloud (the reference uses unseeded rand)."""
+    fr = O.parse_urdf_tree(golden("fridge.urdf"))
+    assert len(fr.link_box) == 7
+    poses, widths = O.fridge_boxes(fr, door_angle=0.0, base=(0, 0, 0))
+    u = O.OracleUnionSDF(poses, widths)
+    rng = np.random.default_rng(0)
+    center, width = np.array([0, 0, 0.75]), np.array([1.5, 1.5, 1.5])
+    for _ in range(20):
+        x = center - 0.5 * width + width * rng.random(3) * 1.5
+        f0 = u(x)
+        num = np.array([(u(x + 1e-6 * e) - f0) / 1e-6 for e in np.eye(3)])
+        assert np.linalg.norm(num - u.gradient(x)) < 1e-4
+
+
+def _fetch_with_spheres(with_base=False):
+    import kinhip
+    tree = O.parse_urdf_tree(golden("fetch.urdf"))
+    om = O.OracleMech(tree, with_base=with_base)
+    sph, rad = [], []
+    for name, c, r in kinhip.FETCH_ARM_SPHERES:
+        sph.append(om.add_new_link(tree.link_id(name), _T(c)))
+        rad.append(r)
+    return tree, om, sph, rad
+
+
+SOLVED = [0.026928521116837873, 0.2378996102914415, 0.6445784881862138, -0.24833437463054583, -1.035118222590030,
+          -0.170439396116480, -1.3891477169766988, -0.07058932825801573]  # test/test_collision.jl:27
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_oracle_collision_fd(with_base):
+    """test/test_collision.jl:18-41: box at (1, 0, 0.8) width 0.3, analytic vs FD gradient, atol 1e-5."""
+    tree, om, sph, rad = _fetch_with_spheres(with_base)
+    ids = [tree.joint_id(n) for n in ARM]
+    box = O.OracleUnionSDF([_T((1.0, 0.0, 0.8))], [[0.3, 0.3, 0.3]])
+    q0 = np.array(SOLVED + ([0.0, 0.0, 0.0] if with_base else []))[:, None]
+    d0, g = O.coll_batch(om, box, q0, ids, sph, rad)
+    eps = 1e-7
+    for i in range(q0.shape[0]):
+        q1 = q0.copy()
+        q1[i] += eps
+        d1, _ = O.coll_batch(om, box, q1, ids, sph, rad, with_grad=False)
+        np.testing.assert_allclose(g[:, i, 0], (d1[:, 0] - d0[:, 0]) / eps, atol=1e-5)
+
+
+# ------------------------------------------------------------------ GPU ------
+def _gpu_setup(with_base=False):
+    import kinhip
+    m = kinhip.parse_urdf(golden("fetch.urdf"), with_base=with_base)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    arm = [m.find_joint(n) for n in ARM]
+    return m, sscc, arm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_gpu_collision_vs_oracle(dtype, with_base):
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(with_base)
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=(1.2, 0.0, 0.0))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    N = 2000
+    g = torch.Generator().manual_seed(5)
+    Q = (torch.rand((8 + (3 if with_base else 0), N), generator=g, dtype=torch.float64) * 3 - 1.5)
+    if with_base:
+        Q[8:] *= 0.3
+    Q = Q.to(dtype).to(dev)
+    plan = sscc.plan(arm, dtype=dtype)
+    D, G, Mn = plan.run(sdf, Q, dists=True, grads=True, min_dist=True)
+    tree, om, sph, rad = _fetch_with_spheres(with_base)
+    box = O.OracleUnionSDF(poses, widths)
+    rd, rg = O.coll_batch(om, box, Q.double().cpu().numpy(), [tree.joint_id(n) for n in ARM], sph, rad)
+    tol = 1e-9 if dtype == torch.float64 else 2e-5
+    np.testing.assert_allclose(D.double().cpu().numpy(), rd, atol=tol)
+    np.testing.assert_allclose(Mn.double().cpu().numpy(), rd.min(0), atol=tol)
+    gd = G.double().cpu().numpy()
+    gtol = 2e-5 if dtype == torch.float64 else 1e-4  # analytic vs the reference's forward difference
+    bad = np.abs(gd - rg) > gtol
+    assert bad.mean() < 1e-3, bad.mean()  # points within ~eps of a box kink differ by construction
+    # single-configuration API
+    m.set_joint_angles(arm, np.r_[SOLVED, [0.0, 0.0, 0.0]] if with_base else np.array(SOLVED))
+    vals, grads = kinhip.compute_coll_dists_and_grads(sscc, arm, sdf)
+    q1 = np.array(SOLVED + ([0.0, 0.0, 0.0] if with_base else []))[:, None]
+    r1, _ = O.coll_batch(om, box, q1, [tree.joint_id(n) for n in ARM], sph, rad)
+    np.testing.assert_allclose(vals, r1[:, 0], atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_collision_fd_and_truncation():
+    """GPU analytic gradient vs central differences of GPU distances (fp64), and truncation_dist."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(with_base=True)
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(_T((1.0, 0.0, 0.8)), [0.3, 0.3, 0.3])])
+    plan = sscc.plan(arm, dtype=torch.float64)
+    q0 = torch.tensor(SOLVED + [0.05, -0.02, 0.1], dtype=torch.float64, device=dev).reshape(-1, 1)
+    eps = 1e-6
+    Qs = q0.repeat(1, 1 + 2 * 11)
+    for i in range(11):
+        Qs[i, 1 + 2 * i] += eps
+        Qs[i, 2 + 2 * i] -= eps
+    D, G, _ = plan.run(sdf, Qs.contiguous(), grads=True)
+    for i in range(11):
+        fd = (D[:, 1 + 2 * i] - D[:, 2 + 2 * i]) / (2 * eps)
+        torch.testing.assert_close(fd, G[:, i, 0], atol=1e-6, rtol=0)
+    D2, G2, _ = plan.run(sdf, q0.contiguous(), grads=True, truncation=0.2)
+    far = D[:, 0] > 0.2
+    assert torch.all(D2[far, 0] == 0.2) and torch.all(G2[far, :, 0] == 0)
+    assert torch.equal(D2[~far, 0], D[~far, 0])
