@@ -246,6 +246,29 @@ KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double trun
                               int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
                               void* stream);
 
+/* ------------------------------------------------------------------------- */
+/* Planning constraints over waypoints (src/planning.jl) */
+/* ------------------------------------------------------------------------- */
+/* IneqConst (src/planning.jl:55-68) for N waypoints (configurations), any
+ * number of trajectories side by side:
+ *   vals [n_spheres][ldv]  min(dist, margin + 0.05) - margin
+ *   jac  [n_spheres][n_q(+3)][ldj]  its gradient (0 where truncated), or NULL
+ * i.e. the reference's val_vec[n_coll*(i-1) + s] and the diagonal block
+ * jac_mat[n_dof*(i-1) + d, n_coll*(i-1) + s] of waypoint i. */
+KINHIP_API int kin_ineq_const_batch(const kin_plan* coll_plan, const kin_sdf* sdf, double margin, const void* q,
+                                    int64_t ldq, int64_t n, void* vals, int64_t ldv, void* jac, int64_t ldj,
+                                    void* stream);
+/* PoseConstraint (src/planning.jl:114-138) of one link for N configurations.
+ * `p` must come from kin_plan_create with n_out = 1, jac_link = that link and
+ * jac_flags = KIN_RPY_JAC | KIN_WITH_ROT (6 rows) or 0 (position only, 3 rows).
+ *   target [12][ldt]  per-configuration target pose (3x4 column-major)
+ *   poses  [12][ldp]  current pose (work + output, required)
+ *   vals   [rows][ldv] [p - p*; rpy - rpy*]
+ *   jac    [n_q(+3)][rows][ldj]  get_jacobian!(..., rpy_jac=true) (kin_plan_run layout; required) */
+KINHIP_API int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, const void* q, int64_t ldq,
+                                    int64_t n, void* poses, int64_t ldp, void* vals, int64_t ldv, void* jac,
+                                    int64_t ldj, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

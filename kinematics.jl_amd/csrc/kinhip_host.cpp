@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -161,6 +162,7 @@ struct kin_model {
 
 struct kin_sdf {
     int32_t n_boxes = 0;
+    int32_t n_aabb = 0;     // the first n_aabb boxes are axis-aligned (KAabb table after the KBox array)
     void* d_f32 = nullptr;
     void* d_f64 = nullptr;
     ~kin_sdf() {
@@ -174,6 +176,7 @@ struct kin_plan {
     int32_t nqcols = 0, rows = 0, ncols = 0, n_q = 0, n_out = 0;
     bool has_jac = false, with_base = false, has_rpy = false;
     bool ik_ok = false;
+    int32_t out_link0 = 0, jac_link = 0;  // first output link / Jacobian link (kin_pose_const_batch)
     std::string ik_why;
     void* d_steps = nullptr;
     KProg<float> pf{};
@@ -640,6 +643,8 @@ struct Stager {
         P.rows = (d.jac_flags & KIN_WITH_ROT) ? 6 : 3;
         P.ncols = has_jac ? d.n_jac + (m.with_base ? 3 : 0) : 0;
         P.has_rpy = (d.jac_flags & KIN_RPY_JAC) != 0;
+        P.out_link0 = d.n_out > 0 ? d.out_link_ids[0] : 0;
+        P.jac_link = has_jac ? d.jac_link_id : 0;
         int32_t pflags = 0;
         if (has_jac) pflags |= PF_JAC;
         if (d.jac_flags & KIN_WITH_ROT) pflags |= PF_WITH_ROT;
@@ -793,6 +798,37 @@ void clear_cache(kin_model* m) {
     m->cache.clear();
 }
 
+}  // namespace
+
+namespace {
+// Signed axis permutation test for a box rotation (columns of R = box axes in
+// the world).  perm[i] = world axis of box axis i.
+bool axis_permutation(const double* pose16, int perm[3]) {
+    int used = 0;
+    for (int i = 0; i < 3; ++i) {
+        perm[i] = -1;
+        for (int j = 0; j < 3; ++j) {
+            const double a = std::fabs(pose16[4 * i + j]);  // column-major: R[j][i]
+            if (a > 1e-12 && std::fabs(a - 1.0) > 1e-12) return false;
+            if (a > 0.5) {
+                if (perm[i] >= 0) return false;
+                perm[i] = j;
+            }
+        }
+        if (perm[i] < 0 || (used & (1 << perm[i]))) return false;
+        used |= 1 << perm[i];
+    }
+    return true;
+}
+
+template <typename T>
+hipError_t upload_boxes(void** dst, const std::vector<KBox<T>>& b, const std::vector<KAabb<T>>& a) {
+    const size_t nb = sizeof(KBox<T>) * b.size(), na = sizeof(KAabb<T>) * a.size();
+    hipError_t e = hipMalloc(dst, nb + na);
+    if (e == hipSuccess) e = hipMemcpy(*dst, b.data(), nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess && na) e = hipMemcpy((char*)*dst + nb, a.data(), na, hipMemcpyHostToDevice);
+    return e;
+}
 }  // namespace
 
 extern "C" {
@@ -954,25 +990,48 @@ int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_id, int32_t
 int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* widths3, kin_sdf** out) {
     if (!out || n_boxes < 1 || !poses16 || !widths3)
         return set_error(KIN_E_INVALID, "kin_sdf_create_boxes: need >= 1 box and non-null arrays");
+    for (int32_t k = 0; k < 3 * n_boxes; ++k)
+        if (!(widths3[k] >= 0)) return set_error(KIN_E_INVALID, "kin_sdf_create_boxes: negative / NaN width");
     auto sd = std::make_unique<kin_sdf>();
     sd->n_boxes = n_boxes;
+    // axis-aligned boxes first (their own order), then the rotated ones
+    std::vector<int32_t> order;
+    std::vector<std::array<int, 3>> perms(n_boxes);
+    for (int32_t k = 0; k < n_boxes; ++k)
+        if (axis_permutation(poses16 + 16 * k, perms[k].data())) order.push_back(k);
+    sd->n_aabb = (int32_t)order.size();
+    for (int32_t k = 0; k < n_boxes; ++k)
+        if (!axis_permutation(poses16 + 16 * k, perms[k].data())) order.push_back(k);
     std::vector<KBox<float>> bf(n_boxes);
     std::vector<KBox<double>> bd(n_boxes);
-    for (int32_t k = 0; k < n_boxes; ++k) {
-        const M34 inv = m_rigid_inverse(m_from_col16(poses16 + 16 * k));  // BoxSDF.inv_pose (src/sdf.jl:60)
-        to_row12<float>(inv, bf[k].inv);
-        to_row12<double>(inv, bd[k].inv);
+    std::vector<KAabb<float>> af(sd->n_aabb);
+    std::vector<KAabb<double>> ad(sd->n_aabb);
+    for (int32_t o = 0; o < n_boxes; ++o) {
+        const int32_t k = order[o];
+        const double* P = poses16 + 16 * k;
+        const M34 inv = m_rigid_inverse(m_from_col16(P));  // BoxSDF.inv_pose (src/sdf.jl:60)
+        to_row12<float>(inv, bf[o].inv);
+        to_row12<double>(inv, bd[o].inv);
         for (int i = 0; i < 3; ++i) {
-            bf[k].half[i] = (float)(0.5 * widths3[3 * k + i]);
-            bd[k].half[i] = 0.5 * widths3[3 * k + i];
+            bf[o].half[i] = (float)(0.5 * widths3[3 * k + i]);
+            bd[o].half[i] = 0.5 * widths3[3 * k + i];
         }
-        bf[k].pad = 0;
-        bd[k].pad = 0;
+        bf[o].pad = 0;
+        bd[o].pad = 0;
+        if (o < sd->n_aabb) {
+            for (int i = 0; i < 3; ++i) {
+                const int j = perms[k][i];  // box axis i lies along world axis j
+                ad[o].c[i] = P[12 + i];
+                af[o].c[i] = (float)P[12 + i];
+                ad[o].half[j] = 0.5 * widths3[3 * k + i];
+                af[o].half[j] = (float)(0.5 * widths3[3 * k + i]);
+            }
+            ad[o].pad[0] = ad[o].pad[1] = 0;
+            af[o].pad[0] = af[o].pad[1] = 0;
+        }
     }
-    hipError_t e = hipMalloc(&sd->d_f32, sizeof(KBox<float>) * n_boxes);
-    if (e == hipSuccess) e = hipMalloc(&sd->d_f64, sizeof(KBox<double>) * n_boxes);
-    if (e == hipSuccess) e = hipMemcpy(sd->d_f32, bf.data(), sizeof(KBox<float>) * n_boxes, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(sd->d_f64, bd.data(), sizeof(KBox<double>) * n_boxes, hipMemcpyHostToDevice);
+    hipError_t e = upload_boxes(&sd->d_f32, bf, af);
+    if (e == hipSuccess) e = upload_boxes(&sd->d_f64, bd, ad);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("kin_sdf_create_boxes: ") + hipGetErrorString(e));
     *out = sd.release();
     return KIN_OK;
@@ -1026,7 +1085,7 @@ int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, con
     if (n == 0) return KIN_OK;
     if ((p->nqcols > 0 && (!q || ldq < n)) || (dists && ldd < n) || (grads && ldg < n))
         return set_error(KIN_E_INVALID, "kin_coll_batch: bad pointer / stride");
-    CollArgs a{truncation, sdf->n_boxes};
+    CollArgs a{truncation, 0.0, sdf->n_boxes, sdf->n_aabb};
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
@@ -1037,6 +1096,53 @@ int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, con
                                 (const KBox<double>*)sdf->d_f64, p->geom, a, (const double*)q, ldq, n, (double*)dists,
                                 ldd, (double*)grads, ldg, (double*)min_dist, (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+
+int kin_ineq_const_batch(const kin_plan* p, const kin_sdf* sdf, double margin, const void* q, int64_t ldq, int64_t n,
+                         void* vals, int64_t ldv, void* jac, int64_t ldj, void* stream) {
+    if (!p || !sdf) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: null plan / sdf");
+    if (!p->is_coll) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: plan was not made by kin_coll_plan_create");
+    if (!std::isfinite(margin)) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: margin must be finite");
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if ((p->nqcols > 0 && (!q || ldq < n)) || !vals || ldv < n || (jac && ldj < n))
+        return set_error(KIN_E_INVALID, "kin_ineq_const_batch: bad pointer / stride");
+    // src/planning.jl:56, :66: truncation_dist = margin + 0.05; val = dist - margin
+    CollArgs a{margin + 0.05, margin, sdf->n_boxes, sdf->n_aabb};
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
+                               (const KBox<float>*)sdf->d_f32, p->geom, a, (const float*)q, ldq, n, (float*)vals, ldv,
+                               (float*)jac, ldj, nullptr, (hipStream_t)stream);
+    else
+        e = launch_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
+                                (const KBox<double>*)sdf->d_f64, p->geom, a, (const double*)q, ldq, n, (double*)vals,
+                                ldv, (double*)jac, ldj, nullptr, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+
+int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, const void* q, int64_t ldq, int64_t n,
+                         void* poses, int64_t ldp, void* vals, int64_t ldv, void* jac, int64_t ldj, void* stream) {
+    if (!p) return set_error(KIN_E_INVALID, "kin_pose_const_batch: null plan");
+    if (p->is_coll || p->n_out != 1 || !p->has_jac || p->out_link0 != p->jac_link)
+        return set_error(KIN_E_INVALID, "kin_pose_const_batch: plan needs n_out = 1 and a Jacobian of that same link");
+    if (p->rows == 6 && !p->has_rpy)
+        return set_error(KIN_E_INVALID, "kin_pose_const_batch: with_rot plans need KIN_RPY_JAC (rpy_jac=true)");
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if (!target || ldt < n || !vals || ldv < n) return set_error(KIN_E_INVALID, "kin_pose_const_batch: bad target / vals");
+    int rc = kin_plan_run(p, q, ldq, n, poses, ldp, jac, ldj, stream);
+    if (rc != KIN_OK) return rc;
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_pose_residual<float>((const float*)poses, ldp, (const float*)target, ldt, n, p->rows, (float*)vals,
+                                        ldv, (hipStream_t)stream);
+    else
+        e = launch_pose_residual<double>((const double*)poses, ldp, (const double*)target, ldt, n, p->rows,
+                                         (double*)vals, ldv, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_pose_residual launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }
 

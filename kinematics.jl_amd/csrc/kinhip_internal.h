@@ -38,12 +38,18 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
 
 struct CollArgs {
     double truncation;
-    int32_t n_boxes;
+    double offset;    // subtracted from every reported distance (IneqConst margin)
+    int32_t n_boxes;  // KBox array (sorted: the first n_aabb are axis-aligned)
+    int32_t n_aabb;   // KAabb array placed right after the KBox array
 };
 
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                        const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
                        int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st);
+
+template <typename T>
+hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,
+                                int64_t ldv, hipStream_t st);
 
 }  // namespace kinhip

@@ -768,25 +768,55 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
 // (the reference takes a forward difference with eps 1e-7, src/sdf.jl:34-41;
 // equal to it up to O(eps) away from the box's kinks).
 // --------------------------------------------------------------------------
+// Monotone surrogate of the box SDF, d*|d|: outside (max q > 0) |max(q,0)|^2,
+// inside -(max q)^2.  The union takes the argmin of the surrogate (no square
+// root per box; sqrt(fl(x*x)) == |x| recovers an inside distance exactly).
 template <typename T>
-__device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, int nb, T px, T py, T pz, T (&gw)[3],
-                                       bool want_grad) {
+__device__ __forceinline__ T box_key(T qx, T qy, T qz) {
+    const T mx = fmax(qx, fmax(qy, qz));
+    const T ox = fmax(qx, T(0)), oy = fmax(qy, T(0)), oz = fmax(qz, T(0));
+    const T oo = fma(ox, ox, fma(oy, oy, oz * oz));
+    return mx > T(0) ? oo : -(mx * mx);
+}
+
+template <typename T, bool GRAD>
+__device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
+                                       int nb, T px, T py, T pz, T (&gw)[3]) {
     T best = T(INFINITY);
     int bk = 0;
-    for (int k = 0; k < nb; ++k) {  // uniform loop, box data through the scalar cache
-        const KBox<T>& b = boxes[k];
-        T qx = fabs(fma(b.inv[0], px, fma(b.inv[1], py, fma(b.inv[2], pz, b.inv[3])))) - b.half[0];
-        T qy = fabs(fma(b.inv[4], px, fma(b.inv[5], py, fma(b.inv[6], pz, b.inv[7])))) - b.half[1];
-        T qz = fabs(fma(b.inv[8], px, fma(b.inv[9], py, fma(b.inv[10], pz, b.inv[11])))) - b.half[2];
-        const T mx = fmax(qx, fmax(qy, qz));
-        const T ox = fmax(qx, T(0)), oy = fmax(qy, T(0)), oz = fmax(qz, T(0));
-        const T d = sqrt_t(ox * ox + oy * oy + oz * oz) + fmin(mx, T(0));
-        if (d < best) {  // argmin: first minimum, as Julia's argmin
-            best = d;
-            bk = k;
+    // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
+#pragma clang loop vectorize(disable) unroll_count(2)
+    for (int k = 0; k < na; ++k) {  // axis-aligned boxes: no rotation
+        const KAabb<T>& b = aabb[k];
+        const T key = box_key(fabs(px - b.c[0]) - b.half[0], fabs(py - b.c[1]) - b.half[1],
+                              fabs(pz - b.c[2]) - b.half[2]);
+        if (GRAD) {
+            if (key < best) {
+                best = key;
+                bk = k;
+            }
+        } else {
+            best = fmin(best, key);
         }
     }
-    if (want_grad) {
+#pragma clang loop vectorize(disable)
+    for (int k = na; k < nb; ++k) {
+        const KBox<T>& b = boxes[k];
+        const T qx = fabs(fma(b.inv[0], px, fma(b.inv[1], py, fma(b.inv[2], pz, b.inv[3])))) - b.half[0];
+        const T qy = fabs(fma(b.inv[4], px, fma(b.inv[5], py, fma(b.inv[6], pz, b.inv[7])))) - b.half[1];
+        const T qz = fabs(fma(b.inv[8], px, fma(b.inv[9], py, fma(b.inv[10], pz, b.inv[11])))) - b.half[2];
+        const T key = box_key(qx, qy, qz);
+        if (GRAD) {
+            if (key < best) {
+                best = key;
+                bk = k;
+            }
+        } else {
+            best = fmin(best, key);
+        }
+    }
+    const T d = best > T(0) ? sqrt_t(best) : -sqrt_t(-best);
+    if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
         const KBox<T>& b = boxes[bk];
         T l[3], q[3], gl[3];
 #pragma unroll
@@ -796,27 +826,26 @@ __device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, int nb
         }
         const T mx = fmax(q[0], fmax(q[1], q[2]));
         if (mx > T(0)) {  // outside: d = |max(q, 0)|
-            const T ox = fmax(q[0], T(0)), oy = fmax(q[1], T(0)), oz = fmax(q[2], T(0));
-            const T nn = sqrt_t(ox * ox + oy * oy + oz * oz);
-            const T o[3] = {ox, oy, oz};
+            const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
+            const T rn = T(1) / sqrt_t(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] = (l[i] < T(0) ? -o[i] : o[i]) / nn;
+            for (int i = 0; i < 3; ++i) gl[i] = (l[i] < T(0) ? -o[i] : o[i]) * rn;
         } else {  // inside: d = max(q)
             const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
 #pragma unroll
             for (int i = 0; i < 3; ++i) gl[i] = (i == im) ? (l[i] < T(0) ? T(-1) : T(1)) : T(0);
         }
-        // world gradient = inv_rot^T * local gradient
 #pragma unroll
         for (int j = 0; j < 3; ++j) gw[j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
     }
-    return best;
+    return d;
 }
 
-template <typename T, int MAXA>
+template <typename T, int MAXA, bool GRAD>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
                                              const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
-                                             const KBox<T>* __restrict__ boxes, int nb, T trunc,
+                                             const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb,
+                                             int na, int nb, T trunc, T offs,
                                              const T (&ro)[MAXA][3], const T (&rz)[MAXA][3], T bx, T by,
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
                                              T* __restrict__ grads, int64_t ldg, T& dmin) {
@@ -827,12 +856,13 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         const T py = fma(f.r[3], sp.c[0], fma(f.r[4], sp.c[1], fma(f.r[5], sp.c[2], f.t[1])));
         const T pz = fma(f.r[6], sp.c[0], fma(f.r[7], sp.c[1], fma(f.r[8], sp.c[2], f.t[2])));
         T g[3] = {T(0), T(0), T(0)};
-        T d = union_sdf(boxes, nb, px, py, pz, g, grads != nullptr) - sp.r;
+        T d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
         const bool cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
         if (cut) d = trunc;
+        d -= offs;  // IneqConst: dist - margin (src/planning.jl:66)
         dmin = fmin(dmin, d);
         if (dists) st_soa(dists, sp.out, ldd, off, d);
-        if (grads) {
+        if (GRAD) {
             const int64_t r0 = (int64_t)sp.out * ndof;
             uint64_t zm = P.zmask;  // q columns that cannot move this chain: 0
             while (zm) {
@@ -874,7 +904,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
     }
 }
 
-template <typename T, int MAXA>
+template <typename T, int MAXA, bool GRAD>
 __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* __restrict__ S,
                                               const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                               const CollArgs a, const T* __restrict__ q, int64_t ldq, int64_t n,
@@ -900,6 +930,7 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
     if (base) base_frame(f, bx, by, bth);
     else set_identity(f);
     const T trunc = (T)a.truncation;
+    const T offs = (T)a.offset;
     T dmin = T(INFINITY);
     T ro[MAXA][3], rz[MAXA][3];
 #pragma unroll
@@ -907,15 +938,58 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
         ro[s][0] = ro[s][1] = ro[s][2] = T(0);
         rz[s][0] = rz[s][1] = rz[s][2] = T(0);
     }
-    coll_spheres<T, MAXA>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, a.n_boxes, trunc, ro, rz, bx, by, off,
+    const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
+    coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs, ro,
+                                rz, bx, by, off,
                           dists, ldd, grads, ldg, dmin);
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         step_a(f, S[s], qa[s], ro[s], rz[s]);
-        coll_spheres<T, MAXA>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, a.n_boxes, trunc, ro, rz, bx, by, off,
+        coll_spheres<T, MAXA, GRAD>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
+                                    offs, ro, rz, bx, by, off,
                               dists, ldd, grads, ldg, dmin);
     }
     if (min_dist) st_soa(min_dist, 0, 0, off, dmin);
+}
+
+// --------------------------------------------------------------------------
+// k_pose_residual: PoseConstraint values (src/planning.jl:125-134)
+//   [t - t*; rpy(R) - rpy(R*)] with rpy = RotZYX angles (src/transform.jl:45-48)
+// from the pose k_fk just wrote; elementwise over configurations.
+// --------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void rpy_zyx(const T (&m)[12], T (&out)[3]) {
+    // m: R11 R21 R31 R12 R22 R32 R13 R23 R33 (column-major 3x3) then t
+    const T t1 = atan2_t(m[1], m[0]);
+    T s1, c1;
+    sincos_t(t1, &s1, &c1);
+    const T t2 = atan2_t(-m[2], fma(m[1], s1, m[0] * c1));
+    const T t3 = atan2_t(fma(m[6], s1, -(m[7] * c1)), fma(m[4], c1, -(m[3] * s1)));
+    out[0] = t3; out[1] = t2; out[2] = t1;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_pose_residual(const T* __restrict__ poses, int64_t ldp,
+                                                       const T* __restrict__ tgt, int64_t ldt, int64_t n, int rows,
+                                                       T* __restrict__ vals, int64_t ldv) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)n) return;
+    const uint32_t off = i * (uint32_t)sizeof(T);
+    T a[12], b[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        a[k] = ld_soa(poses, k, ldp, off);
+        b[k] = ld_soa(tgt, k, ldt, off);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st_soa(vals, k, ldv, off, a[9 + k] - b[9 + k]);
+    if (rows == 6) {
+        T ra[3], rb[3];
+        rpy_zyx(a, ra);
+        rpy_zyx(b, rb);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) st_soa(vals, 3 + k, ldv, off, ra[k] - rb[k]);
+    }
 }
 
 inline unsigned grid_of(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
@@ -1016,9 +1090,29 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
         T* gc = grads ? grads + s0 : grads;
         T* mc = min_dist ? min_dist + s0 : min_dist;
 #define KIN_CO_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_coll<T, MA>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
-        KIN_MAXA_DISPATCH(g.maxA, KIN_CO_LAUNCH)
+        hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
+#define KIN_COG_LAUNCH(MA) \
+        hipLaunchKernelGGL((k_coll<T, MA, true>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
+        if (grads) {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_COG_LAUNCH)
+        } else {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_CO_LAUNCH)
+        }
 #undef KIN_CO_LAUNCH
+#undef KIN_COG_LAUNCH
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+template <typename T>
+hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,
+                                int64_t ldv, hipStream_t st) {
+    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        const int64_t c = std::min(kChunk, n - s0);
+        hipLaunchKernelGGL((k_pose_residual<T>), dim3(grid_of(c, 256)), dim3(256), 0, st, poses + s0, ldp, target + s0,
+                           ldt, c, rows, vals + s0, ldv);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1035,7 +1129,9 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
                                            int64_t, T*, int64_t, int64_t, hipStream_t);                      \
     template hipError_t launch_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,   \
                                        const LaunchGeom&, const CollArgs&, const T*, int64_t, int64_t, T*,    \
-                                       int64_t, T*, int64_t, T*, hipStream_t);
+                                       int64_t, T*, int64_t, T*, hipStream_t);                                \
+    template hipError_t launch_pose_residual<T>(const T*, int64_t, const T*, int64_t, int64_t, int, T*, int64_t, \
+                                                hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

@@ -70,6 +70,17 @@ struct KBox {
     T pad;
 };
 
+// A box whose rotation is a signed axis permutation, as a world-axis-aligned
+// box: |R^T (p - t)| is a permutation of |p - t|, so the SDF needs only the
+// centre and the permuted half widths (kin_sdf_create_boxes sorts these boxes
+// first and stores them in this compact form after the KBox array).
+template <typename T>
+struct KAabb {
+    T c[3];
+    T half[3];
+    T pad[2];
+};
+
 template <typename T>
 struct KProg {
     int32_t nA;        // phase-A steps (root -> spine link, padded to the kernel's MAXA)

@@ -14,8 +14,12 @@ from .mechanism import (  # noqa: F401
 )
 from .synth import uniform_configs  # noqa: F401
 from .collision import (  # noqa: F401
-    FETCH_ARM_SPHERES, BoxSDF, CollisionPlan, SweptSphereCollisionChecker, UnionSDF, add_fetch_arm_spheres,
-    compute_coll_dists, compute_coll_dists_and_grads, fridge_sdf,
+    FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, BoxSDF, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
+    add_coll_links, add_fetch_arm_spheres, compute_coll_dists, compute_coll_dists_and_grads, fridge_sdf,
+)
+from .planning import (  # noqa: F401
+    ConfigurationConstraint, EqConst, IneqConst, Objective, PoseConstraint, construct_problem,
+    create_straight_trajectory, plan_trajectory,
 )
 
 FETCH_ARM_JOINTS = [

@@ -35,6 +35,7 @@ EXPORTS = [
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
+    "kin_ineq_const_batch", "kin_pose_const_batch",
 ]
 
 
@@ -115,6 +116,8 @@ def lib():
         "kin_sdf_destroy": ([P], C.c_int),
         "kin_coll_plan_create": ([P, P, P], C.c_int),
         "kin_coll_batch": ([P, P, C.c_double, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
+        "kin_ineq_const_batch": ([P, P, C.c_double, P, I64, I64, P, I64, P, I64, P], C.c_int),
+        "kin_pose_const_batch": ([P, P, I64, P, I64, I64, P, I64, P, I64, P, I64, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -165,6 +165,22 @@ FETCH_ARM_SPHERES = [
 ]
 
 
+# per-link table used by add_coll_links (the arm spheres above plus the torso column)
+FETCH_LINK_SPHERES: dict = {}
+for _name, _c, _r in FETCH_ARM_SPHERES + [("torso_lift_link", (-0.08, 0.0, z), 0.16) for z in (0.15, 0.35, 0.55)]:
+    FETCH_LINK_SPHERES.setdefault(_name, []).append((_c, _r))
+
+
+def add_coll_links(sscc: SweptSphereCollisionChecker, coll_link: Link, spheres=None):
+    """src/collision.jl:39-49: attach the swept spheres of `coll_link` as CollSphere links.
+    The reference computes them from the link's collision mesh (skrobot + trimesh, offline-
+    unavailable); here they come from `spheres` [(centre, radius), ...] or the build-defined
+    FETCH_LINK_SPHERES table (KeyError for a link it does not cover)."""
+    for c, r in (spheres if spheres is not None else FETCH_LINK_SPHERES[coll_link.name]):
+        sscc.add_coll_sphere(coll_link, c, r)
+    return sscc
+
+
 def add_fetch_arm_spheres(sscc: SweptSphereCollisionChecker):
     for name, c, r in FETCH_ARM_SPHERES:
         sscc.add_coll_sphere(sscc.mech.find_link(name), c, r)

@@ -1,0 +1,252 @@
+"""Trajectory-optimisation constraints over waypoints (src/planning.jl) on the GPU.
+
+SURVEY.md 8f row f3.  The constraint evaluations -- the serial inner loop of
+``plan_trajectory`` in the reference (one ``set_joint_angles`` +
+``compute_coll_dists_and_grads`` per waypoint, src/planning.jl:59-67) -- run as
+ONE batched launch over all waypoints (of one or many trajectories):
+
+* ``IneqConst``  -> ``kin_ineq_const_batch`` (k_coll with truncation
+  ``margin + 0.05`` and the ``- margin`` offset fused in);
+* ``PoseConstraint`` -> ``kin_pose_const_batch`` (k_fk with rpy Jacobian +
+  k_pose_residual).
+
+The optimiser stays on the host, as the reference's does: ``Objective``,
+``ConfigurationConstraint``, ``EqConst`` are small host-side assemblies and
+``plan_trajectory`` drives SciPy's SLSQP (the reference's ``solver=:SCIPY``
+path).  NLopt and Ipopt are not available offline; ``solver="NLOPT"`` runs the
+same SLSQP algorithm (Kraft's, which NLopt's LD_SLSQP also wraps) with NLopt's
+bounds and ``ftol_abs`` semantics and reports NLopt-style status symbols.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib as K
+from .collision import SweptSphereCollisionChecker, UnionSDF
+from .mechanism import Link, Mechanism, _device
+
+_DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
+
+
+# ---------------------------------------------------------------------------- host side
+class Objective:
+    """src/planning.jl:1-28: xi^T A xi with A = kron(A_acc, diag(w^2)) (finite-difference acceleration)."""
+
+    def __init__(self, n_wp: int, weights):
+        from scipy import sparse
+        w = np.asarray(weights, np.float64)
+        A_sub = np.zeros((n_wp, n_wp))
+        blk = np.array([[1, -2, 1], [-2, 4, -2], [1, -2, 1]], np.float64)
+        for i in range(1, n_wp - 1):
+            A_sub[i - 1:i + 2, i - 1:i + 2] += blk
+        self.A = sparse.csc_matrix(np.kron(A_sub, np.diag(w ** 2)))
+        self.n_dim = self.A.shape[1]
+
+    def __call__(self, xi, grad: Optional[np.ndarray] = None) -> float:
+        tmp = self.A @ np.asarray(xi, np.float64)
+        if grad is not None and len(grad) > 0:
+            grad[:] = 2.0 * tmp
+        return float(np.dot(xi, tmp))
+
+
+class IneqConst:
+    """src/planning.jl:32-68.  ``__call__(xi, val_vec, jac_mat)`` fills the reference's dense
+    layout (val_vec [n_coll*n_wp], jac_mat [n_dof*n_wp, n_coll*n_wp], block diagonal) from one
+    GPU launch over the n_wp waypoints; ``eval_batch`` is the device-resident batched form."""
+
+    def __init__(self, sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, n_wp: int, margin: float,
+                 dtype=torch.float64):
+        self.sscc, self.joints, self.sdf = sscc, list(joints), sdf
+        self.n_wp = int(n_wp)
+        self.n_dof = len(self.joints) + (3 if sscc.mech.with_base else 0)
+        self.n_coll = len(sscc.sphere_links)
+        self.n_cons = self.n_coll * self.n_wp
+        self.margin = float(margin)
+        self.plan = sscc.plan(self.joints, dtype=dtype)
+        self.dtype = dtype
+        self.jac_mat = np.zeros((self.n_dof * self.n_wp, self.n_cons))
+        self.val_vec = np.zeros(self.n_cons)
+
+    def eval_batch(self, Q: torch.Tensor, with_jac=True, stream=None):
+        """Q: device [n_dof, N] (any number of waypoints / trajectories side by side) ->
+        vals [n_coll, N], jac [n_coll, n_dof, N] (or None).  Async on the stream."""
+        if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
+            raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
+        N = Q.shape[1]
+        V = torch.empty((self.n_coll, N), dtype=self.dtype, device=Q.device)
+        G = torch.empty((self.n_coll, self.n_dof, N), dtype=self.dtype, device=Q.device) if with_jac else None
+        st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+        K.check(K.lib().kin_ineq_const_batch(self.plan._h, self.sdf._h, self.margin, Q.data_ptr(), Q.stride(0), N,
+                                             V.data_ptr(), N, G.data_ptr() if G is not None else None, N, st))
+        return V, G
+
+    def __call__(self, xi, val_vec: np.ndarray, jac_mat: np.ndarray):
+        xi = np.asarray(xi, np.float64)
+        Q = torch.tensor(xi.reshape(self.n_wp, self.n_dof).T.copy(), dtype=self.dtype, device=_device())
+        V, G = self.eval_batch(Q)
+        v = V.double().cpu().numpy()    # [n_coll, n_wp]
+        g = G.double().cpu().numpy()    # [n_coll, n_dof, n_wp]
+        nd, nc = self.n_dof, self.n_coll
+        for i in range(self.n_wp):
+            jac_mat[nd * i:nd * (i + 1), nc * i:nc * (i + 1)] = g[:, :, i].T
+        val_vec[:] = v.T.reshape(-1)
+
+
+class PartialConstraint:
+    idx_wp: int
+    n_dof: int
+    n_cons: int
+
+
+class ConfigurationConstraint(PartialConstraint):
+    """src/planning.jl:72-88: q(idx_wp) == q_const."""
+
+    def __init__(self, idx_wp: int, n_dof: int, q_const):
+        self.idx_wp, self.n_dof, self.n_cons = int(idx_wp), int(n_dof), int(n_dof)
+        self.q_const = np.asarray(q_const, np.float64)
+
+    def __call__(self, q, val_vec, jac_mat):
+        j0 = (self.idx_wp - 1) * self.n_dof
+        jac_mat[j0:j0 + self.n_dof, :] = -np.eye(self.n_dof)
+        val_vec[:] = self.q_const - np.asarray(q, np.float64)
+
+
+class PoseConstraint(PartialConstraint):
+    """src/planning.jl:90-138: pose of each move link at waypoint idx_wp == target
+    (position, plus rpy when with_rot); Jacobian = get_jacobian!(..., rpy_jac=true)."""
+
+    def __init__(self, idx_wp: int, n_dof: int, move_links, target_poses, with_rots, mech: Mechanism, joints,
+                 dtype=torch.float64):
+        if isinstance(move_links, Link):
+            move_links, target_poses, with_rots = [move_links], [target_poses], [with_rots]
+        self.idx_wp, self.n_dof = int(idx_wp), int(n_dof)
+        self.move_links, self.with_rots = list(move_links), [bool(w) for w in with_rots]
+        self.target_poses = [np.asarray(T, np.float64).reshape(4, 4) for T in target_poses]
+        self.n_cons = sum(6 if w else 3 for w in self.with_rots)
+        self.mech, self.joints, self.dtype = mech, list(joints), dtype
+        self.plans = [mech.plan(self.joints, out_links=[l], jac_link=l, jac_joints=self.joints, with_rot=w,
+                                rpy_jac=w, dtype=dtype) for l, w in zip(self.move_links, self.with_rots)]
+
+    def eval_batch(self, k: int, Q: torch.Tensor, targets: torch.Tensor, stream=None):
+        """Move link k for N configurations: Q [n_dof, N], targets [12, N] (3x4 column-major) ->
+        (vals [dim, N], jac [n_dof, dim, N], poses [12, N]) on the device."""
+        p = self.plans[k]
+        dim = 6 if self.with_rots[k] else 3
+        N = Q.shape[1]
+        if Q.dtype != self.dtype or not Q.is_cuda or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
+            raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
+        if targets.dtype != self.dtype or targets.shape != (12, N) or targets.stride(1) != 1:
+            raise ValueError("targets must be (12, N) in the plan dtype")
+        P = torch.empty((12, N), dtype=self.dtype, device=Q.device)
+        V = torch.empty((dim, N), dtype=self.dtype, device=Q.device)
+        J = torch.empty((self.n_dof, dim, N), dtype=self.dtype, device=Q.device)  # zero-filled plan
+        st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+        K.check(K.lib().kin_pose_const_batch(p._h, targets.data_ptr(), targets.stride(0), Q.data_ptr(), Q.stride(0),
+                                             N, P.data_ptr(), N, V.data_ptr(), N, J.data_ptr(), N, st))
+        return V, J, P
+
+    def __call__(self, q, val_vec, jac_mat):
+        dev = _device()
+        Q = torch.tensor(np.asarray(q, np.float64), dtype=self.dtype, device=dev).reshape(-1, 1).contiguous()
+        j0 = (self.idx_wp - 1) * self.n_dof
+        i0 = 0
+        for k, (T, w) in enumerate(zip(self.target_poses, self.with_rots)):
+            tg = torch.tensor(np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]]), dtype=self.dtype,
+                              device=dev).reshape(12, 1)
+            V, J, _ = self.eval_batch(k, Q, tg)
+            dim = 6 if w else 3
+            val_vec[i0:i0 + dim] = V[:, 0].double().cpu().numpy()
+            # get_jacobian!(..., transpose(jac)): jac_mat[j0 + d, i0 + r] = J[r, d]; irrelevant
+            # columns are left untouched, as get_jacobian! leaves them
+            Jh = J[:, :, 0].double().cpu().numpy()  # [n_dof, dim]
+            rel = [self.mech.is_relevant(j, self.move_links[k]) for j in self.joints]
+            rel += [True] * (self.n_dof - len(self.joints))
+            for d in range(self.n_dof):
+                if rel[d]:
+                    jac_mat[j0 + d, i0:i0 + dim] = Jh[d]
+            i0 += dim
+
+
+class EqConst:
+    """src/planning.jl:140-176: stacked partial constraints."""
+
+    def __init__(self, n_wp: int, cons_arr: Sequence[PartialConstraint]):
+        self.n_dof = cons_arr[0].n_dof
+        assert all(c.n_dof == self.n_dof for c in cons_arr)
+        self.n_wp, self.cons_arr = int(n_wp), list(cons_arr)
+        self.n_cons = sum(c.n_cons for c in cons_arr)
+        self.jac_mat = np.zeros((self.n_dof * self.n_wp, self.n_cons))
+        self.val_vec = np.zeros(self.n_cons)
+
+    def __call__(self, xi, val_vec, jac_mat):
+        X = np.asarray(xi, np.float64).reshape(self.n_wp, self.n_dof)
+        i0 = 0
+        for c in self.cons_arr:
+            c(X[c.idx_wp - 1], val_vec[i0:i0 + c.n_cons], jac_mat[:, i0:i0 + c.n_cons])
+            i0 += c.n_cons
+
+
+def create_straight_trajectory(q_start, q_goal, n_wp: int) -> np.ndarray:
+    """src/planning.jl:304-308."""
+    q_start, q_goal = np.asarray(q_start, np.float64), np.asarray(q_goal, np.float64)
+    step = (q_goal - q_start) / (n_wp - 1)
+    return np.concatenate([q_start + step * i for i in range(n_wp)])
+
+
+def construct_problem(sscc, joints, sdf, q_start, q_goal, n_wp, n_dof, margin, partial_consts=()):
+    """src/planning.jl:310-330."""
+    eq = [ConfigurationConstraint(1, n_dof, q_start), ConfigurationConstraint(n_wp, n_dof, q_goal)]
+    eq += list(partial_consts)
+    return (Objective(n_wp, np.ones(n_dof)), IneqConst(sscc, joints, sdf, n_wp, margin), EqConst(n_wp, eq),
+            n_dof * n_wp)
+
+
+def plan_trajectory(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, q_start, q_goal, n_wp: int,
+                    margin=2e-2, partial_consts=(), ftol_abs=1e-3, solver="NLOPT", maxiter=200):
+    """src/planning.jl:332-401 -> (q_seq [n_dof, n_wp], status).  Constraint evaluations on the GPU."""
+    from scipy.optimize import minimize
+    from .collision import compute_coll_dists
+
+    solver = str(solver).lstrip(":").upper()
+    if solver not in ("NLOPT", "SCIPY"):
+        raise ValueError(f"solver {solver!r} is not available (NLopt-compatible SLSQP and SCIPY are)")
+    m = sscc.mech
+    n_dof = len(joints) + (3 if m.with_base else 0)
+    assert len(q_start) == n_dof and len(q_goal) == n_dof
+    for q in (q_start, q_goal):
+        m.set_joint_angles(joints, q)
+        assert np.all(compute_coll_dists(sscc, joints, sdf) > 0.0), "start / goal in collision"
+    xi0 = create_straight_trajectory(q_start, q_goal, n_wp)
+    F, G, H, n_whole = construct_problem(sscc, joints, sdf, q_start, q_goal, n_wp, n_dof, margin, partial_consts)
+
+    def cached(cons):  # one GPU evaluation per iterate serves both fun and jac
+        last = {}
+
+        def ev(x):
+            key = x.tobytes()
+            if last.get("key") != key:
+                cons(x, cons.val_vec, cons.jac_mat)
+                last.update(key=key, val=cons.val_vec.copy(), jac=cons.jac_mat.T.copy())
+            return last
+        return (lambda x: ev(x)["val"]), (lambda x: ev(x)["jac"])
+
+    g_val, g_jac = cached(G)
+    h_val, h_jac = cached(H)
+    grad = np.zeros(n_whole)
+    cons = [{"type": "ineq", "fun": g_val, "jac": g_jac}, {"type": "eq", "fun": h_val, "jac": h_jac}]
+    bounds = None
+    if solver == "NLOPT":
+        lo = [j.lower_limit for j in joints] + ([-np.inf] * 3 if m.with_base else [])
+        hi = [j.upper_limit for j in joints] + ([np.inf] * 3 if m.with_base else [])
+        bounds = list(zip(lo * n_wp, hi * n_wp))
+    res = minimize(lambda x: F(x, grad), xi0, jac=lambda x: (F(x, grad), grad.copy())[1], method="SLSQP",
+                   bounds=bounds, constraints=cons, options={"ftol": ftol_abs, "maxiter": maxiter})
+    q_seq = res.x.reshape(n_wp, n_dof).T
+    if solver == "SCIPY":
+        return q_seq, res
+    status = ":FTOL_REACHED" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")
+    return q_seq, status

@@ -401,3 +401,38 @@ def fridge_boxes(tree: UrdfTree, door_angle=2.0, base=(1.2, 0.0, 0.0)):
         poses.append(m.get_transform(lid) @ org)
         widths.append(ext)
     return np.array(poses), np.array(widths)
+
+
+# ---------------------------------------------------------------------------
+# Planning constraints (src/planning.jl), restated on top of the functions above
+# ---------------------------------------------------------------------------
+def ineq_const(mech: "OracleMech", sdf: OracleUnionSDF, xi, q_joint_ids, sphere_links, radii, n_wp, margin):
+    """IneqConst(xi, val_vec, jac_mat), src/planning.jl:55-68: per waypoint i the spheres'
+    dists (truncated at margin + 0.05) minus margin, and the block-diagonal jac_mat
+    [n_dof*n_wp, n_coll*n_wp] of their gradients."""
+    xi = np.asarray(xi, np.float64)
+    n_dof = xi.size // n_wp
+    Q = xi.reshape(n_wp, n_dof).T  # reshape(xi, (n_dof, n_wp)), column-major
+    d, g = coll_batch(mech, sdf, Q, q_joint_ids, sphere_links, radii, truncation=margin + 0.05)
+    n_coll = d.shape[0]
+    val = np.zeros(n_coll * n_wp)
+    jac = np.zeros((n_dof * n_wp, n_coll * n_wp))
+    for i in range(n_wp):
+        jac[n_dof * i:n_dof * (i + 1), n_coll * i:n_coll * (i + 1)] = g[:, :, i].T
+        val[n_coll * i:n_coll * (i + 1)] = d[:, i] - margin
+    return val, jac
+
+
+def pose_const(mech: "OracleMech", q, q_joint_ids, link_id, target4x4, with_rot):
+    """PoseConstraint for one link, src/planning.jl:114-138: [p - p*; rpy - rpy*] and the
+    rpy Jacobian (get_jacobian!(..., rpy_jac=true)) as [dim, n_dof]."""
+    q = np.asarray(q, np.float64).reshape(-1, 1)
+    ids = list(q_joint_ids)
+    pose, J = mech.fk_jac_batch(q, ids, link_id, ids, with_rot=with_rot, rpy_jac=True)
+    cur = np.eye(4)
+    cur[:3, :] = pose[:, 0].reshape(4, 3).T
+    T = np.asarray(target4x4, np.float64)
+    diff = cur[:3, 3] - T[:3, 3]
+    if with_rot:
+        diff = np.concatenate([diff, rpy(cur) - rpy(T)])
+    return diff, J[:, :, 0].T  # J: [ncol, rows, 1] -> [rows, ncol]

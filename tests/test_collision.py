@@ -161,3 +161,33 @@ def test_gpu_collision_fd_and_truncation():
     far = D[:, 0] > 0.2
     assert torch.all(D2[far, 0] == 0.2) and torch.all(G2[far, :, 0] == 0)
     assert torch.equal(D2[~far, 0], D[~far, 0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gpu_collision_box_kinds(dtype):
+    """Axis-permuted boxes (stored as world-aligned boxes) mixed with generally rotated ones, in an
+    order where the tie-breaking first-minimum is irrelevant; distances and gradients vs the oracle."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    rx = np.array([[1, 0, 0], [0, 0, -1], [0, 1, 0]], float)     # 90 deg about x
+    rz = np.array([[0, 1, 0], [-1, 0, 0], [0, 0, 1]], float)     # -90 deg about z
+    ang = 0.7
+    rg = _rotz(ang) @ np.array([[1, 0, 0], [0, np.cos(0.4), -np.sin(0.4)], [0, np.sin(0.4), np.cos(0.4)]])
+    poses = [_T((0.6, 0.3, 0.9), rg), _T((0.7, -0.2, 0.5), rx), _T((0.4, 0.5, 1.2), rz), _T((0.9, 0.0, 0.2)),
+             _T((0.5, -0.6, 1.0), rz @ rx)]
+    widths = [[0.2, 0.3, 0.1], [0.3, 0.15, 0.4], [0.1, 0.5, 0.2], [0.6, 0.6, 0.05], [0.2, 0.1, 0.3]]
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    N = 3000
+    g = torch.Generator().manual_seed(9)
+    Q = (torch.rand((8, N), generator=g, dtype=torch.float64) * 3 - 1.5).to(dtype).to(dev)
+    D, G, Mn = sscc.plan(arm, dtype=dtype).run(sdf, Q, grads=True, min_dist=True)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    rd, rgr = O.coll_batch(om, O.OracleUnionSDF(poses, widths), Q.double().cpu().numpy(),
+                           [tree.joint_id(n) for n in ARM], sph, rad)
+    tol = 1e-9 if dtype == torch.float64 else 2e-5
+    np.testing.assert_allclose(D.double().cpu().numpy(), rd, atol=tol)
+    np.testing.assert_allclose(Mn.double().cpu().numpy(), rd.min(0), atol=tol)
+    bad = np.abs(G.double().cpu().numpy() - rgr) > (2e-5 if dtype == torch.float64 else 1e-4)
+    assert bad.mean() < 1e-3, bad.mean()
