@@ -154,10 +154,20 @@ def _coll_leg(ctx, stream, n, steps):
     return out
 
 
-def _cpu_baseline(m, N_budget_s=12.0):
-    """Reference-faithful C restatement (oracle/kin_oracle.c) on the host cores, bounded sample."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_baseline(m, N_budget_s=12.0, single_s=4.0):
+    """Reference-faithful C restatement (oracle/kin_oracle.c) on the host cores, bounded sample:
+    all-threads run (the reported value) and a 1-thread run (1 core and all cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle as O
 
     tree = O.parse_urdf_tree(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
@@ -169,16 +179,40 @@ def _cpu_baseline(m, N_budget_s=12.0):
     chunk = 1 << 16
     q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], chunk,
                                dtype=torch.float64).numpy()
-    om.fk_jac_batch(q[:, :1024], ids, gl, ids, True, False, n_threads=threads)  # warm
-    done, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < N_budget_s:
-        om.fk_jac_batch(q, ids, gl, ids, True, False, n_threads=threads)
-        done += chunk
-    dt = time.perf_counter() - t0
+
+    def run(nthr, budget, n):
+        om.fk_jac_batch(q[:, :1024], ids, gl, ids, True, False, n_threads=nthr)  # warm
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            om.fk_jac_batch(q[:, :n], ids, gl, ids, True, False, n_threads=nthr)
+            done += n
+        return done, time.perf_counter() - t0
+
+    done, dt = run(threads, N_budget_s, chunk)
+    d1, t1 = run(1, single_s, 4096)
     return {"value": done / dt, "unit": "evals/s", "cores": threads, "kind": "port",
+            "single_core_value": d1 / t1, "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"{done} Fetch configs (chunks of {chunk}) through or_fk_jac_batch: per-config "
                       f"Mechanism state, cache invalidate, quaternion joint transforms, dense 4x4 fp64 "
-                      f"(src/algorithm.jl restated), {threads} OpenMP threads, {dt:.1f} s"}
+                      f"(src/algorithm.jl restated), {threads} OpenMP threads, {dt:.1f} s; plus {d1} configs "
+                      f"on 1 thread in {t1:.1f} s"}
+
+
+def _copy_bw(dev, nbytes=1 << 31):
+    """Device-to-device copy rate (read + write bytes / s) as the practical HBM ceiling."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * 10 / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
 
 
 def _pmc_traffic():
@@ -198,7 +232,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=1 << 20, help="configurations per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--extras", type=int, default=1, help="also time fp64 FK+J and config-2 FK")
+    ap.add_argument("--extras", type=int, default=1, help="also time fp64 FK+J, config 2, IK and collision legs")
+    ap.add_argument("--row-pad", type=int, default=256, help="elements of padding per SoA row (ld = n + pad)")
+    ap.add_argument("--sweep", action="store_true", help="batch-size sweep, unpadded rows, strong scaling")
     args = ap.parse_args()
 
     ctx = D.init_from_env()
@@ -210,13 +246,18 @@ def main():
     lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
     stream = torch.cuda.Stream(dev)
 
-    def leg(dtype, jac, links):
+    def leg(dtype, jac, links, n=N, pad=args.row_pad):
+        """Device-resident SoA buffers; every row padded to ld = n + pad elements (the C-ABI's
+        ldq / ldp / ldj): rows exactly 2^k elements apart line all 68 streams of a wave up on the
+        same HBM channels (tools/ld_probe.py, profiles/r01_row_pad_probe.txt)."""
         plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
                       with_rot=True, dtype=dtype)
-        Q = kinhip.uniform_configs(lo, hi, N, start=rank * N, dtype=dtype, device=dev)
-        poses = torch.empty((len(links), 12, N), dtype=dtype, device=dev)
-        J = torch.empty((8, 6, N), dtype=dtype, device=dev) if jac else None
-        return plan, Q, poses, J
+        ld = n + pad
+        Qb = torch.empty((8, ld), dtype=dtype, device=dev)
+        Qb[:, :n] = kinhip.uniform_configs(lo, hi, n, start=rank * n, dtype=dtype, device=dev)
+        poses = torch.empty((len(links), 12, ld), dtype=dtype, device=dev)[:, :, :n]
+        J = torch.empty((8, 6, ld), dtype=dtype, device=dev)[:, :, :n] if jac else None
+        return plan, Qb[:, :n], poses, J
 
     # ---- headline: FK + J, fp32 -------------------------------------------------
     plan, Q, poses, J = leg(torch.float32, True, [gl])
@@ -241,6 +282,32 @@ def main():
                      "kernel": "k_fk<float,8>", "algorithmic_bytes_per_eval": bytes_per_eval,
                      "avg_launch_us": t_launch * 1e6},
     }
+    out["config"]["row_pad_elems"] = args.row_pad
+    if args.extras:
+        out["roofline"]["measured_copy_GBs"] = _copy_bw(dev)
+    if args.sweep:
+        # batch sweep: launch-overhead vs bandwidth regime, fp32 FK + J
+        sweep = {}
+        for lg in range(16, 27, 2):
+            for pad in (0, args.row_pad):
+                n_s = 1 << lg
+                ps, Qs, Ps, Js = leg(torch.float32, True, [gl], n=n_s, pad=pad)
+                k_s = max(5, min(50, (1 << 26) // n_s))
+                ws_, ds_ = _time_plan(ps, Qs, Ps, Js, k_s, 3, ctx, stream)
+                sweep[f"2^{lg}+{pad}"] = {"evals_per_s": n_s * ws * k_s / ws_, "avg_launch_us": ds_ / k_s * 1e6,
+                                          "achieved_GBs": bytes_per_eval * n_s / (ds_ / k_s) / 1e9}
+                del ps, Qs, Ps, Js
+        out["batch_sweep_fk_jac_f32"] = sweep
+        if ws > 1:  # strong scaling: one global 2^20 batch split across the ranks
+            st0, cnt = D.split_range(N, rank, ws)
+            ps = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+            Qs = kinhip.uniform_configs(lo, hi, cnt, start=st0, dtype=torch.float32, device=dev)
+            Ps = torch.empty((1, 12, cnt), dtype=torch.float32, device=dev)
+            Js = torch.empty((8, 6, cnt), dtype=torch.float32, device=dev)
+            w_s, d_s = _time_plan(ps, Qs, Ps, Js, args.steps, args.warmup, ctx, stream)
+            out["strong_scaling_fk_jac_f32"] = {"global_batch": N, "value": N * args.steps / w_s, "unit": "evals/s",
+                                                "ms_per_step": w_s / args.steps * 1e3}
+            del ps, Qs, Ps, Js
     if args.extras:
         # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
         p64, Q64, P64, J64 = leg(torch.float64, True, [gl])

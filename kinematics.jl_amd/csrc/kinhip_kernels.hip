@@ -310,6 +310,22 @@ __device__ __forceinline__ void emit_jcol(const JacCtx<T>& J, const KStep<T>& st
     }
 }
 
+// Block -> configuration chunk.  Workgroups are dispatched round-robin over the
+// 8 XCDs (block b on XCD b % 8); with KINHIP_XCD_REMAP each XCD instead takes
+// one contiguous eighth of the batch, so its L2 and DRAM pages see sequential
+// row segments rather than every eighth 1 KB piece.
+#ifndef KINHIP_XCD_REMAP
+#define KINHIP_XCD_REMAP 0
+#endif
+__device__ __forceinline__ uint32_t config_block() {
+#if KINHIP_XCD_REMAP
+    const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7u, q = nb >> 3, r = nb & 7u;
+    return x * q + (x < r ? x : r) + (b >> 3);
+#else
+    return blockIdx.x;
+#endif
+}
+
 // --------------------------------------------------------------------------
 // k_fk: batched get_transform (any set of links) + get_jacobian! of one link
 // --------------------------------------------------------------------------
@@ -321,7 +337,7 @@ __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* slots = reinterpret_cast<T*>(smem);
     const int B = blockDim.x, tid = threadIdx.x;
-    const uint32_t i = blockIdx.x * (uint32_t)B + tid;
+    const uint32_t i = config_block() * (uint32_t)B + tid;
     if (i >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
     const uint32_t off = i * (uint32_t)sizeof(T);
     Sink<T> sk;

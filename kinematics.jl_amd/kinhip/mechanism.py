@@ -268,14 +268,13 @@ class Plan:
         if jac is None and self._jl:
             alloc = torch.zeros if not self.zero_fill else torch.empty
             jac = alloc((self.jac_cols, self.jac_rows, N), dtype=self.dtype, device=dev)
-        for t, shape in ((poses, (self.n_out, 12, N)), (jac, (self.jac_cols, self.jac_rows, N))):
-            if t is not None and (tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != self.dtype):
-                raise ValueError(f"output must be a contiguous {self.dtype} tensor of shape {shape}")
+        ldp = _ld_of(poses, (self.n_out, 12, N), self.dtype) if poses is not None else N
+        ldj = _ld_of(jac, (self.jac_cols, self.jac_rows, N), self.dtype) if jac is not None else N
         st = (stream or torch.cuda.current_stream(dev)).cuda_stream
         ldq = Q.stride(0) if self.n_qcols else N
         K.check(K.lib().kin_plan_run(self._h, Q.data_ptr() if self.n_qcols else None, ldq, N,
-                                     poses.data_ptr() if poses is not None else None, N,
-                                     jac.data_ptr() if jac is not None else None, N, st))
+                                     poses.data_ptr() if poses is not None else None, ldp,
+                                     jac.data_ptr() if jac is not None else None, ldj, st))
         return poses, jac
 
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
@@ -399,6 +398,18 @@ def get_joint_angles(m: Mechanism, joints):
 
 def add_new_link(m: Mechanism, new_link: Link, parent: Link, pose_or_position):
     return m.add_new_link(new_link, parent, pose_or_position)
+
+
+def _ld_of(t: torch.Tensor, shape, dtype) -> int:
+    """Leading dimension of a [a][b][ld] SoA output given as a (possibly row-padded) view of shape
+    `shape` = (a, b, N): configuration stride 1, rows `ld` apart (the C-ABI's ldp / ldj)."""
+    if tuple(t.shape) != tuple(shape) or t.dtype != dtype or not t.is_cuda:
+        raise ValueError(f"output must be a CUDA {dtype} tensor of shape {tuple(shape)}")
+    a, b, n = shape
+    ld = t.stride(1) if b > 1 else (t.stride(0) if a > 1 else n)
+    if t.stride(2) != 1 or ld < n or (a > 1 and t.stride(0) != b * ld):
+        raise ValueError("output rows must be evenly spaced with unit configuration stride")
+    return ld
 
 
 def _device():

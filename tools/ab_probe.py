@@ -1,0 +1,39 @@
+"""One variant's FK + J fp32 timings (used by tools/ab_xcd.sh; KINHIP_LIB selects the build)."""
+import os
+import sys
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
+import kinhip  # noqa: E402
+
+dev = torch.device("cuda", 0)
+m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
+gl = m.find_link("gripper_link")
+plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
+res = []
+CASES = [tuple(map(int, c.split(":"))) for c in os.environ.get("AB_CASES", "20:0,20:256,22:0,24:0,24:256").split(",")]
+for lg, pad in CASES:
+    N = 1 << lg
+    ld = N + pad
+    Qb = torch.empty((8, ld), dtype=torch.float32, device=dev)
+    Qb[:, :N] = kinhip.uniform_configs(lo, hi, N, dtype=torch.float32, device=dev)
+    Q = Qb[:, :N]
+    P = torch.empty((1, 12, ld), dtype=torch.float32, device=dev)[:, :, :N]
+    J = torch.empty((8, 6, ld), dtype=torch.float32, device=dev)[:, :, :N]
+    for _ in range(10):
+        plan.run(Q, P, J)
+    torch.cuda.synchronize()
+    k = max(20, (1 << 27) // N)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(k):
+        plan.run(Q, P, J)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / k * 1e3
+    res.append(f"2^{lg}+{pad}: {us:7.2f}us {272 * N / us / 1e3:6.0f}GB/s")
+    del Qb, P, J
+print(os.path.basename(os.environ.get("KINHIP_LIB", "default")).ljust(24), " | ".join(res), flush=True)

@@ -13,9 +13,10 @@ sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac64", "fk6_64", "ik32", "ik64"])
+ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac64", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--n", type=int, default=1 << 20)
+ap.add_argument("--pad", type=int, default=256, help="row padding of the SoA buffers (as bench.py)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
@@ -23,10 +24,14 @@ arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
 gl = m.find_link("gripper_link")
 dt = torch.float64 if a.what.endswith("64") else torch.float32
 Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], a.n, dtype=dt, device=dev)
+ld = a.n + a.pad
 if a.what.startswith("fkjac"):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
-    P = torch.empty((1, 12, a.n), dtype=dt, device=dev)
-    J = torch.empty((8, 6, a.n), dtype=dt, device=dev)
+    Qb = torch.empty((8, ld), dtype=dt, device=dev)
+    Qb[:, :a.n] = Q
+    Q = Qb[:, :a.n]
+    P = torch.empty((1, 12, ld), dtype=dt, device=dev)[:, :, :a.n]
+    J = torch.empty((8, 6, ld), dtype=dt, device=dev)[:, :, :a.n]
     for _ in range(a.steps):
         plan.run(Q, P, J)
 elif a.what == "fk6_64":
@@ -36,6 +41,14 @@ elif a.what == "fk6_64":
     P = torch.empty((6, 12, a.n), dtype=dt, device=dev)
     for _ in range(a.steps):
         plan.run(Q, P)
+elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge scene
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    sdf = kinhip.fridge_sdf(fr)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    cp = sscc.plan(arm, dtype=dt)
+    grads = a.what.startswith("collg")
+    for _ in range(a.steps):
+        cp.run(sdf, Q, dists=grads, grads=grads, min_dist=not grads)
 else:
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     T, _ = plan.run(Q)

@@ -11,3 +11,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 tail -1 gpurun_out/bench_rocprof.log
 bash tools/prof_session.sh fkjac32 || exit 5
 bash tools/prof_session.sh fkjac64 || exit 6
+bash tools/prof_session.sh coll32 || exit 7
+bash tools/prof_session.sh collg32 || exit 8
+timeout -k 10 600 python bench.py --no-cpu --sweep --steps 20 > gpurun_out/bench_sweep.json 2> gpurun_out/bench_sweep.err || { tail gpurun_out/bench_sweep.err; exit 9; }

@@ -22,7 +22,28 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "fkjac32": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20), "FK + 6x8 J, fp32, N = 2^20: 8 q in, 60 out"),
     "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
     "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
+    "coll32": ("k_coll<float, 8, false>", (8 + 1) * 4 * (1 << 20),
+               "config 5 validity: FK + 14 spheres vs 7-box fridge SDF, min distance out, fp32, N = 2^20"),
+    "collg32": ("k_coll<float, 8, true>", (8 + 14 + 14 * 8) * 4 * (1 << 20),
+                "config 5 / IneqConst: 14 distances + 14x8 gradients out, fp32, N = 2^20"),
 }
+N_CU, N_SIMD = 256, 4
+
+
+def valu_metrics(c):
+    """VALU utilisation from the SQ counters (gfx94x formulas; MI355X_MICROARCH.md: SQ_ACTIVE_INST_*
+    count quad-cycles, GRBM_GUI_ACTIVE is summed over the 8 XCDs)."""
+    if "GRBM_GUI_ACTIVE" not in c:
+        return {}
+    cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+    out = {"elapsed_cycles": cyc}
+    if "SQ_ACTIVE_INST_VALU" in c:
+        out["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (N_CU * N_SIMD) / cyc
+    if "SQ_INSTS_VALU" in c:  # wave64 fp32 VALU op = 2 cycles on a SIMD (SIMD-32 issue)
+        out["valu_issue_frac_fp32"] = c["SQ_INSTS_VALU"] * 2 / (N_CU * N_SIMD) / cyc
+        if "SQ_WAVES" in c:
+            out["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+    return out
 
 
 def counters(tag):
@@ -65,6 +86,7 @@ def main():
              "avg_duration_ns_trace": float(st["AverageNs"]) if st else None,
              "achieved_GBs_trace": (alg / float(st["AverageNs"])) if st else None,
              "sq": {k: v for k, v in c.items() if k.startswith(("SQ_", "GRBM_"))},
+             "valu": valu_metrics(c),
              "method": "rocprofv3 --kernel-trace --stats, then separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ_*), "
                        "20 launches each via tools/prof_kernel.py; hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950)"}
         with open(os.path.join(OUT, f"{a.round}_pmc_{tag}.json"), "w") as f:
