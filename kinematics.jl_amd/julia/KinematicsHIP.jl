@@ -207,6 +207,101 @@ function point_inverse_kinematics_nakamura!(hm::HIPModel, link::Link, joints::Ve
     Q
 end
 
-export HIPModel, point_inverse_kinematics_nakamura!
+# --- collision (src/sdf.jl, src/collision.jl) and planning constraints (src/planning.jl) ---
+
+struct KinCollDesc
+    dtype::Int32
+    n_q::Int32
+    q_joint_ids::Ptr{Int32}
+    n_spheres::Int32
+    sphere_link_ids::Ptr{Int32}
+    centers::Ptr{Float64}
+    radii::Ptr{Float64}
+end
+
+"""Device copy of a UnionSDF of BoxSDFs (or a single BoxSDF)."""
+mutable struct HIPSDF
+    handle::Ptr{Cvoid}
+end
+
+function HIPSDF(sdf::Kinematics.AbstractSDF)
+    boxes = sdf isa Kinematics.UnionSDF ? sdf.sdfs : [sdf]
+    poses = Float64[]
+    widths = Float64[]
+    for b in boxes
+        append!(poses, vec(Matrix(b.pose.mat)))
+        append!(widths, collect(b.width))
+    end
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:kin_sdf_create_boxes, libkinhip), Cint, (Int32, Ptr{Float64}, Ptr{Float64}, Ref{Ptr{Cvoid}}),
+                length(boxes), poses, widths, h))
+    s = HIPSDF(h[])
+    finalizer(x -> ccall((:kin_sdf_destroy, libkinhip), Cint, (Ptr{Cvoid},), x.handle), s)
+    s
+end
+
+function coll_plan!(hm::HIPModel, ::Type{T}, sscc::Kinematics.SweptSphereCollisionChecker,
+                    joints::Vector{<:Joint}) where {T}
+    ids = Int32[j.id for j in joints]
+    sph = Int32[l.id for l in sscc.sphere_links]
+    key = (:coll, T, ids, sph)
+    get!(hm.plans, key) do
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        r = Float64.(sscc.sphere_radii)
+        GC.@preserve ids sph r begin
+            d = KinCollDesc(dtype_code(T), length(ids), pointer(ids), length(sph), pointer(sph), C_NULL, pointer(r))
+            check(ccall((:kin_coll_plan_create, libkinhip), Cint, (Ptr{Cvoid}, Ref{KinCollDesc}, Ref{Ptr{Cvoid}}),
+                        hm.handle, d, h))
+        end
+        h[]
+    end
+end
+
+"""Batched `compute_coll_dists_and_grads!`: vals (N, n_spheres), grads (N, n_dof, n_spheres) for every row of Q.
+`hm` must be built after the spheres were added (`add_coll_links`)."""
+function compute_coll_dists_and_grads!(hm::HIPModel, sscc::Kinematics.SweptSphereCollisionChecker,
+                                       joints::Vector{<:Joint}, sdf::HIPSDF, Q::ROCMatrix{T},
+                                       vals::ROCMatrix{T}, grads::Union{Nothing,ROCArray{T,3}};
+                                       truncation_dist=Inf) where {T}
+    N = size(Q, 1)
+    p = coll_plan!(hm, T, sscc, joints)
+    check(ccall((:kin_coll_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Float64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{T},
+                 Ptr{Cvoid}),
+                p, sdf.handle, truncation_dist, pointer(Q), stride(Q, 2), N, pointer(vals), N,
+                grads === nothing ? C_NULL : pointer(grads), N, C_NULL, stream_ptr()))
+    vals, grads
+end
+
+"""IneqConst over every waypoint column of Xi (N = waypoints of one or many trajectories, rows = dof):
+vals (N, n_coll) = min(dist, margin + 0.05) - margin, jac (N, n_dof, n_coll)."""
+function ineq_const!(hm::HIPModel, sscc::Kinematics.SweptSphereCollisionChecker, joints::Vector{<:Joint},
+                     sdf::HIPSDF, margin::Real, Xi::ROCMatrix{T}, vals::ROCMatrix{T}, jac::ROCArray{T,3}) where {T}
+    N = size(Xi, 1)
+    p = coll_plan!(hm, T, sscc, joints)
+    check(ccall((:kin_ineq_const_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Float64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
+                p, sdf.handle, Float64(margin), pointer(Xi), stride(Xi, 2), N, pointer(vals), N, pointer(jac), N,
+                stream_ptr()))
+    vals, jac
+end
+
+"""PoseConstraint of one link for N configurations: targets (N, 12), vals (N, 6 or 3), jac (N, dim, dof)."""
+function pose_const!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool, targets::ROCMatrix{T},
+                     Q::ROCMatrix{T}, vals::ROCMatrix{T}, jac::ROCArray{T,3}) where {T}
+    N = size(Q, 1)
+    ids = Int32[j.id for j in joints]
+    flags = with_rot ? (KIN_WITH_ROT | KIN_RPY_JAC) : UInt32(0)
+    p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, flags | KIN_ZERO_FILL)
+    poses = ROCArray{T}(undef, N, 12)
+    check(ccall((:kin_pose_const_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{T}, Int64,
+                 Ptr{Cvoid}),
+                p, pointer(targets), stride(targets, 2), pointer(Q), stride(Q, 2), N, pointer(poses), N,
+                pointer(vals), N, pointer(jac), N, stream_ptr()))
+    vals, jac
+end
+
+export HIPModel, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
 
 end # module
