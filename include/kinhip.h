@@ -200,6 +200,9 @@ typedef struct kin_ik_params {
                            attempt re-draws the relevant joints uniformly within their limits
                            (U[-pi, pi] if unbounded) from a counter hash of (seed, i, attempt, column) */
     uint64_t seed;
+    int32_t lanes;      /* lanes per target running attempts side by side: 0 = auto, else 1/2/4/8.
+                           Results are identical for every value (each attempt's arithmetic is the
+                           sequential schedule's); only the parallelism changes. */
 } kin_ik_params;
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,

@@ -1155,8 +1155,10 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
     if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0) || prm->restarts < 0)
         return set_error(KIN_E_INVALID, "bad IK parameters");
+    if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
+        return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
     IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-             prm->restarts, prm->seed};
+             prm->restarts, prm->seed, prm->lanes};
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,

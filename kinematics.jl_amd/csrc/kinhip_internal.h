@@ -25,6 +25,7 @@ struct IkArgs {
     int32_t with_rot;
     int32_t restarts;
     uint64_t seed;
+    int32_t lanes;  // 0 auto
 };
 
 template <typename T>

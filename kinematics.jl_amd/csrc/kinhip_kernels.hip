@@ -21,6 +21,9 @@
 // HBM-bound at the sizes of BASELINE.json (roofline).
 #include <hip/hip_runtime.h>
 
+#include <climits>
+#include <cstdlib>
+
 #include <algorithm>
 
 #include "kinhip_internal.h"
@@ -514,6 +517,7 @@ struct IkArgsT {
     int32_t max_iters;
     T lam2, tol_pos, tol_rot, max_step;
     int32_t attempt_len;  // 0: no restarts
+    int32_t n_attempts;   // 1 + (max_iters - 1) / attempt_len (attempts the sequential schedule reaches)
     uint64_t seed;
     int64_t ibase;  // global index of this chunk's first configuration
 };
@@ -530,16 +534,53 @@ __device__ __forceinline__ double ik_seed_u01(uint64_t seed, int64_t i, int32_t 
 
 // --------------------------------------------------------------------------
 // k_ik_dls: batched damped least squares, dq = J^T (J J^T + lambda^2 I)^-1 e
+//
+// Restart schedule (kin_ik_params): attempt 0 starts from q0 and is checked at
+// iterations 0..L; attempt k >= 1 starts from seeded random angles at
+// iteration kL + 1 and ends at (k+1)L (the last one at max_iters); the answer
+// is the first attempt that converges.  Attempts are independent, so G lanes
+// of one wave share a target and run attempts slot, slot + G, ... side by side
+// (G = 1: the plain sequential loop).  Each lane's arithmetic is exactly the
+// sequential schedule's; a lane stops once a lower attempt of its target has
+// converged, and the lowest converged attempt (else the last one) is written.
+// Small batches (65k targets = one wave per SIMD) gain G x the parallelism.
 // --------------------------------------------------------------------------
-template <typename T, int MAXA, int ROWS>
-__global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>* __restrict__ S,
+template <typename T, int MAXA>
+__device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S, const IkArgsT<T>& a,
+                                                 const T* __restrict__ q, int64_t ldq, uint32_t off, int64_t gi,
+                                                 int att, T (&qs)[MAXA]) {
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const KStep<T>& st = S[s];
+        const int32_t c = st.qcol;
+        T v = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
+        if (att > 0 && c >= 0) {
+            if (st.flags & SF_REC) {
+                double lo = (double)st.lo, hi = (double)st.hi;
+                if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
+                v = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, c));
+            } else {
+                v = fmin(fmax(v, st.lo), st.hi);  // attempt 0's first step has clamped it
+            }
+        }
+        qs[s] = v;
+    }
+}
+
+#ifndef KINHIP_IK_WAVES
+#define KINHIP_IK_WAVES 1
+#endif
+template <typename T, int MAXA, int ROWS, int G>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_WAVES))) void k_ik_dls(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                 const IkArgsT<T> a, const T* __restrict__ tgt, int64_t ldt,
                                                 T* __restrict__ q, int64_t ldq, int64_t n,
                                                 int32_t* __restrict__ iters, T* __restrict__ err,
                                                 int64_t lde) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)n) return;
-    const uint32_t off = i * (uint32_t)sizeof(T);
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = gt / G;  // target (lanes of one target are adjacent: same wave)
+    const int slot = (int)(gt % G);
+    const bool valid = i < (uint64_t)n;
+    const uint32_t off = (valid ? i : 0u) * (uint32_t)sizeof(T);
     T Rt[9], pt[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -547,49 +588,65 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
         for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
         pt[r] = ld_soa(tgt, 9 + r, ldt, off);
     }
-    T qs[MAXA];
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        qs[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
-    }
     const bool base = (P.flags & PF_BASE) != 0;
-    T b[3] = {T(0), T(0), T(0)};
+    T b0[3] = {T(0), T(0), T(0)};
     if (base)
-        for (int k = 0; k < 3; ++k) b[k] = ld_soa(q, P.base_col + k, ldq, off);
-    const T b0[3] = {b[0], b[1], b[2]};
+        for (int k = 0; k < 3; ++k) b0[k] = ld_soa(q, P.base_col + k, ldq, off);
+    const int64_t gi = a.ibase + (int64_t)i;
+    const int L = a.attempt_len;
 
-    int it = 0;
+    int att = slot;
+    bool done = !valid || att >= a.n_attempts;
+    int res_att = INT_MAX;  // attempt at which this lane converged
+    bool final_lane = false;
+    T qs[MAXA], b[3] = {b0[0], b0[1], b0[2]};
+    int it = att > 0 ? att * L + 1 : 0;
+    ik_start_attempt<T, MAXA>(S, a, q, ldq, off, gi, att, qs);
     T ep = 0, er = 0;
     T ro[MAXA][3], rz[MAXA][3];
-    for (;; ++it) {
-        Fr<T> root, L;
+    for (;;) {
+        if constexpr (G > 1) {  // lowest converged attempt of this target so far
+            int gm = res_att;
+#pragma unroll
+            for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
+            if (!done && gm < att) done = true;
+        }
+        if (__ballot(!done) == 0) break;  // wave-uniform exit: every lane finished or superseded
+        if (done) continue;
+        Fr<T> root, L_;
         if (base) base_frame(root, b[0], b[1], b[2]);
         else set_identity(root);
-        chain_records<T, MAXA>(P, S, root, qs, L, ro, rz);
+        chain_records<T, MAXA>(P, S, root, qs, L_, ro, rz);
+        const Fr<T>& Lf = L_;
         T e[6];
-        e[0] = pt[0] - L.t[0]; e[1] = pt[1] - L.t[1]; e[2] = pt[2] - L.t[2];
+        e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
         ep = sqrt_t(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
         er = T(0);
         if constexpr (ROWS == 6) {
             T w[3];
-            rot_error(Rt, L.r, w);
+            rot_error(Rt, Lf.r, w);
             e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
             er = sqrt_t(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
-        if ((ep < a.tol_pos && er < a.tol_rot) || it >= a.max_iters) break;
-        if (a.attempt_len > 0 && it > 0 && it % a.attempt_len == 0) {  // restart (see kin_ik_params)
-            const int32_t att = it / a.attempt_len;
-#pragma unroll
-            for (int s = 0; s < MAXA; ++s) {
-                const KStep<T>& st = S[s];
-                if (st.qcol >= 0 && (st.flags & SF_REC)) {
-                    double lo = (double)st.lo, hi = (double)st.hi;
-                    if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
-                    qs[s] = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, a.ibase + (int64_t)i, att, st.qcol));
-                }
+        if (ep < a.tol_pos && er < a.tol_rot) {
+            res_att = att;
+            done = true;
+            continue;
+        }
+        if (it >= a.max_iters) {  // only the last attempt gets here
+            final_lane = true;
+            done = true;
+            continue;
+        }
+        if (L > 0 && it > 0 && it % L == 0) {  // attempt over: this lane's next one, if any
+            att += G;
+            if (att >= a.n_attempts) {
+                done = true;
+            } else {
+                it = att * L + 1;
+                ik_start_attempt<T, MAXA>(S, a, q, ldq, off, gi, att, qs);
+                b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
             }
-            for (int k = 0; k < 3; ++k) b[k] = b0[k];
             continue;
         }
 
@@ -601,8 +658,8 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
                 for (int r = 0; r < ROWS; ++r) Jb[k][r] = T(0);
             Jb[0][0] = T(1);
             Jb[1][1] = T(1);
-            Jb[2][0] = -(L.t[1] - b[1]);
-            Jb[2][1] = L.t[0] - b[0];
+            Jb[2][0] = -(Lf.t[1] - b[1]);
+            Jb[2][1] = Lf.t[0] - b[0];
             if constexpr (ROWS == 6) Jb[2][5] = T(1);
         }
         // pass 0: every joint; pass 1 (lanes that need it): joints sitting on a
@@ -623,7 +680,7 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], L, J);
+                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) J[r] *= w[s];
 #pragma unroll
@@ -675,7 +732,7 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], L, J);
+                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
                 T v = T(0);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
@@ -704,7 +761,18 @@ __global__ __launch_bounds__(256) void k_ik_dls(const KProg<T> P, const KStep<T>
         for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(qs[s] + sc * dq[s], S[s].lo), S[s].hi);
         if (base)
             for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
+        ++it;
     }
+    bool writer = final_lane;
+    if constexpr (G > 1) {
+        int gm = res_att;
+#pragma unroll
+        for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
+        writer = (gm != INT_MAX) ? (res_att == gm) : final_lane;
+    } else {
+        writer = valid;
+    }
+    if (!writer) return;
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
@@ -1046,24 +1114,47 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
     return hipSuccess;
 }
 
+// Lanes per IK target (parallel restart attempts): enough to put ~8 waves on
+// every SIMD for small batches, never more than the attempts the schedule has.
+// KINHIP_IK_GROUP=<1|2|4|8> overrides (A/B).
+static int ik_group(int64_t n, int n_attempts, int lanes) {
+    static const int env = [] {
+        const char* e = getenv("KINHIP_IK_GROUP");
+        return e ? atoi(e) : 0;
+    }();
+    const int forced = lanes ? lanes : env;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
+    int g = 1;
+    while (g < n_attempts && g < 8 && n * g * 2 <= (int64_t(1) << 19)) g *= 2;
+    return g;
+}
+
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
                          int64_t lde, hipStream_t st) {
-    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step),
-                  a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0, a.seed, 0};
-    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+    const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
+    const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
+    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
+                  0};
+    const int G = ik_group(n, natt, a.lanes);
+    const int64_t chunk = kChunk / 8;  // lane index gt = i * G stays below 2^32
+    for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = s0;
-        const int64_t c = std::min(kChunk, n - s0);
-        const dim3 grid(grid_of(c, 256)), block(256);
+        const int64_t c = std::min(chunk, n - s0);
+        const dim3 grid(grid_of(c * G, 256)), block(256);
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
+#define KIN_IK_G(MA, R, GG) \
+        hipLaunchKernelGGL((k_ik_dls<T, MA, R, GG>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
 #define KIN_IK6(MA) \
-        hipLaunchKernelGGL((k_ik_dls<T, MA, 6>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
+        switch (G) { case 2: KIN_IK_G(MA, 6, 2); break; case 4: KIN_IK_G(MA, 6, 4); break; \
+                     case 8: KIN_IK_G(MA, 6, 8); break; default: KIN_IK_G(MA, 6, 1); }
 #define KIN_IK3(MA) \
-        hipLaunchKernelGGL((k_ik_dls<T, MA, 3>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
+        switch (G) { case 2: KIN_IK_G(MA, 3, 2); break; case 4: KIN_IK_G(MA, 3, 4); break; \
+                     case 8: KIN_IK_G(MA, 3, 8); break; default: KIN_IK_G(MA, 3, 1); }
         if (a.with_rot) {
             KIN_MAXA_DISPATCH(g.maxA, KIN_IK6)
         } else {
@@ -1071,6 +1162,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         }
 #undef KIN_IK6
 #undef KIN_IK3
+#undef KIN_IK_G
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

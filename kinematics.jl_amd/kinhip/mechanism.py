@@ -278,15 +278,16 @@ class Plan:
         return poses, jac
 
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-               max_step=0.5, with_rot=True, restarts=0, seed=0, stream=None):
-        """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N])."""
+               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, stream=None):
+        """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
+        target running restart attempts side by side (0 auto; results identical for every value)."""
         N = self._check_q(Q)
         if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
             raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
         iters = torch.empty(N, dtype=torch.int32, device=Q.device)
         err = torch.empty((2, N), dtype=self.dtype, device=Q.device)
         prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
-                         int(restarts), int(seed))
+                         int(restarts), int(seed), int(lanes))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         K.check(K.lib().kin_ik_dls_batch(self._h, C.byref(prm), targets.data_ptr(), N, Q.data_ptr(), Q.stride(0), N,
                                          iters.data_ptr(), err.data_ptr(), N, st))

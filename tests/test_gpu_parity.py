@@ -280,8 +280,10 @@ def test_ik_dls_iterates_vs_oracle(dev, fetch_tree):
         np.testing.assert_array_equal(it.cpu().numpy(), rit)
 
 
-def test_ik_dls_restarts_vs_oracle(dev, fetch_tree):
-    """Restart re-seeding (counter hash of seed, index, attempt, column) identical on both sides."""
+@pytest.mark.parametrize("lanes", [0, 1, 2, 4, 8])
+def test_ik_dls_restarts_vs_oracle(dev, fetch_tree, lanes):
+    """Restart re-seeding (counter hash of seed, index, attempt, column) identical on both sides,
+    whether the attempts run in one lane or side by side in 2/4/8 lanes of a target."""
     m, arm = _fetch()
     gl = m.find_link("gripper_link")
     ids = [j.id for j in arm]
@@ -291,11 +293,37 @@ def test_ik_dls_restarts_vs_oracle(dev, fetch_tree):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
     Q = torch.zeros((8, N), dtype=torch.float64, device=dev)
     Q, it, err = plan.ik_dls(torch.tensor(tgt, device=dev).contiguous(), Q, max_iters=13, restarts=3, seed=77,
-                             tol_pos=1e-12, tol_rot=1e-12)
+                             tol_pos=1e-12, tol_rot=1e-12, lanes=lanes)
     rq, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, max_iters=13, restarts=3, seed=77,
                                  tol_pos=1e-12, tol_rot=1e-12)
     np.testing.assert_array_equal(it.cpu().numpy(), rit)
     np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ik_dls_lanes_identical(dev, fetch_tree, dtype):
+    """Converging runs where the winning attempt varies by target: every lanes-per-target setting
+    returns bit-identical angles, iteration counts and errors, and fp64 matches the oracle."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 2000
+    tgt = _targets(om, ids, gl.id, N, 33)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
+    res = []
+    for lanes in (1, 2, 4, 8):
+        Q = torch.zeros((8, N), dtype=dtype, device=dev)
+        res.append(plan.ik_dls(T, Q, max_iters=23, restarts=4, seed=5, lam=1e-2, max_step=0.5, lanes=lanes))
+    it0 = res[0][1].cpu().numpy()
+    assert len(set((it0 // 4).tolist())) > 2  # winners spread over several attempts (attempt length 4)
+    for Q, it, err in res[1:]:
+        assert torch.equal(Q, res[0][0]) and torch.equal(it, res[0][1]) and torch.equal(err, res[0][2])
+    if dtype == torch.float64:
+        rq, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, max_iters=23, restarts=4, seed=5)
+        np.testing.assert_array_equal(it0, rit)
+        np.testing.assert_allclose(res[0][0].cpu().numpy(), rq, atol=1e-7)
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
