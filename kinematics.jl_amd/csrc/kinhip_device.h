@@ -1,0 +1,355 @@
+// kinhip_device.h -- device helpers shared by the gfx950 (MI355X / CDNA4)
+// kernels of the batched kinematics engine (kinhip_fk.hip, kinhip_ik.hip,
+// kinhip_coll.hip).  Compiled only for --offload-arch=gfx950.
+//
+// Reference semantics (HiroIshida/Kinematics.jl):
+//   k_fk        get_transform over many links + get_jacobian!  (src/algorithm.jl:1-106,
+//               joint_transform src/mechanism.jl:90-103, rpy src/transform.jl:45-48)
+//   k_ik_dls    batched damped-least-squares replacement of the SLSQP loop of
+//               inverse_kinematics! (src/inverse_kinematics.jl:23-64), build-defined
+//   k_nakamura  point_inverse_kinematics_nakamura (src/algorithm.jl:116-131)
+//   k_coll      compute_coll_dists_and_grads! (src/collision.jl:51-94, src/sdf.jl)
+//   k_pose_residual  PoseConstraint values (src/planning.jl:114-138)
+//
+// Execution model: one configuration per lane (wave64).  Joint angles, poses
+// and Jacobians are SoA with the configuration index fastest, so every load
+// and store of a wave touches 64 consecutive elements (256 B fp32 / 512 B
+// fp64).  The staged program (kinhip_prog.h) is identical for every lane: its
+// fields are read with uniform addresses (scalar loads through the scalar
+// cache), and its control flow is wave-uniform.  The root -> Jacobian-link
+// chain ("phase A", <= MAXA steps) is fully unrolled so that the per-joint
+// world origins/axes the Jacobian needs stay in registers; other links are
+// evaluated by a uniform loop that branches through per-lane LDS slots.
+// No MFMA: 3x4 rigid products are not a dense contraction; the kernels are
+// HBM-bound at the sizes of BASELINE.json (roofline).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdlib>
+
+#include <algorithm>
+
+#include "kinhip_internal.h"
+
+
+
+
+namespace kinhip {
+namespace {
+
+template <typename T>
+struct Fr {
+    T r[9];  // row-major rotation
+    T t[3];
+};
+
+// sin/cos of joint angles.  The library sincos carries a Payne-Hanek
+// reduction for huge arguments that, inlined once per joint, dominates the
+// kernel's code and register budget.  Joint angles are small, so: Cody-Waite
+// reduction by pi/2 with FMA-split constants, minimax kernels on [-pi/4, pi/4]
+// (Cephes sinf/cosf for fp32, fdlibm __kernel_sin/__kernel_cos for fp64), and
+// the library call kept only behind a rarely taken |x| bound.
+__device__ __noinline__ void sincos_slow(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __noinline__ void sincos_slow(double x, double* s, double* c) { sincos(x, s, c); }
+
+__device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
+    if (__builtin_expect(!(fabsf(x) < 8192.0f), 0)) {
+        sincos_slow(x, s, c);
+        return;
+    }
+    const float j = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-j, 1.57079637050628662109375f, x);
+    r = fmaf(-j, -4.37113900018624283e-8f, r);
+    const float z = r * r;
+    const float sp = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float cp = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                          fmaf(-0.5f, z, 1.0f));
+    const int qd = (int)j & 3;
+    const float ss = (qd & 1) ? cp : sp, cc = (qd & 1) ? sp : cp;
+    *s = (qd & 2) ? -ss : ss;
+    *c = ((qd + 1) & 2) ? -cc : cc;
+}
+
+__device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
+    if (__builtin_expect(!(fabs(x) < 1048576.0), 0)) {
+        sincos_slow(x, s, c);
+        return;
+    }
+    const double j = rint(x * 0.63661977236758134308);
+    double r = fma(-j, 1.57079632679489655800e+00, x);
+    r = fma(-j, 6.12323399573676603587e-17, r);
+    r = fma(-j, -1.49738490485916983e-33, r);
+    const double z = r * r;
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                                  2.75573137070700676789e-06),
+                                        -1.98412698298579493134e-04),
+                              8.33333333332248946124e-03),
+                          -1.66666666666666324348e-01);
+    const double sp = fma(r * z, ps, r);
+    const double pc = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                   -2.75573143513906633035e-07),
+                                         2.48015872894767294178e-05),
+                               -1.38888888888741095749e-03),
+                           4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cp = w + (((1.0 - w) - hz) + z * pc);
+    const int qd = (int)(long long)j & 3;
+    const double ss = (qd & 1) ? cp : sp, cc = (qd & 1) ? sp : cp;
+    *s = (qd & 2) ? -ss : ss;
+    *c = ((qd + 1) & 2) ? -cc : cc;
+}
+__device__ __forceinline__ float atan2_t(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double atan2_t(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float sqrt_t(float x) { return sqrtf(x); }
+__device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
+
+// SoA addressing: element `row` of a [rows][ld] array for this lane.  Each
+// row gets a wave-uniform buffer descriptor (SGPRs: base = row pointer) and
+// every load/store uses the same 32-bit lane byte offset (one VGPR), i.e.
+// `buffer_load/store_dword v, v_off, s[rsrc], 0 offen` -- no 64-bit per-access
+// address arithmetic in VGPRs.  The launcher splits batches (kChunk) so lane
+// byte offsets stay below 2^31.  KINHIP_STORE_AUX selects the cache policy of
+// the output stream (0 = default, 2 = nt: +10% on the FK+J stream, A/B in
+// profiles/r01_ab_variants.txt).
+#ifndef KINHIP_STORE_AUX
+#define KINHIP_STORE_AUX 2
+#endif
+typedef unsigned int u32x2 __attribute__((__vector_size__(8)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float ld_soa(const float* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base + row * ld), (int)off, 0, 0));
+}
+__device__ __forceinline__ double ld_soa(const double* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base + row * ld), (int)off, 0, 0));
+}
+__device__ __forceinline__ void st_soa(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base + row * ld), (int)off, 0, KINHIP_STORE_AUX);
+}
+__device__ __forceinline__ void st_soa(double* __restrict__ base, int64_t row, int64_t ld, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), row_rsrc(base + row * ld), (int)off, 0,
+                                          KINHIP_STORE_AUX);
+}
+
+template <typename T>
+__device__ __forceinline__ void set_identity(Fr<T>& f) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f.r[k] = (k % 4 == 0) ? T(1) : T(0);
+    f.t[0] = f.t[1] = f.t[2] = T(0);
+}
+
+// f <- f * F   (F: row-major 3x4 in uniform memory)
+template <typename T>
+__device__ __forceinline__ void mul_rigid(Fr<T>& f, const T* __restrict__ F) {
+    const T F0 = F[0], F1 = F[1], F2 = F[2], F3 = F[3];
+    const T F4 = F[4], F5 = F[5], F6 = F[6], F7 = F[7];
+    const T F8 = F[8], F9 = F[9], F10 = F[10], F11 = F[11];
+    Fr<T> g;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
+        g.r[3 * i + 0] = fma(a, F0, fma(b, F4, c * F8));
+        g.r[3 * i + 1] = fma(a, F1, fma(b, F5, c * F9));
+        g.r[3 * i + 2] = fma(a, F2, fma(b, F6, c * F10));
+        g.t[i] = fma(a, F3, fma(b, F7, fma(c, F11, f.t[i])));
+    }
+    f = g;
+}
+
+template <typename T>
+__device__ __forceinline__ void mul_rigid_regs(Fr<T>& out, const Fr<T>& f, const T (&F)[12]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
+        out.r[3 * i + 0] = fma(a, F[0], fma(b, F[4], c * F[8]));
+        out.r[3 * i + 1] = fma(a, F[1], fma(b, F[5], c * F[9]));
+        out.r[3 * i + 2] = fma(a, F[2], fma(b, F[6], c * F[10]));
+        out.t[i] = fma(a, F[3], fma(b, F[7], fma(c, F[11], f.t[i])));
+    }
+}
+
+// joint motion in the canonical frame (axis = local z), branch-free in the
+// joint kind: revolute -> (c, s, 0), prismatic -> (1, 0, scale*q), none -> (1, 0, 0)
+template <typename T>
+__device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T scale, T qv) {
+    const bool rev = kind == MOT_REV;
+    T th = rev ? qv : T(0);
+    if (flags & SF_SCALE) {  // UnitQuaternion normalisation of a non-unit axis
+        T sh, ch;
+        sincos_t(T(0.5) * qv, &sh, &ch);
+        th = T(2) * atan2_t(scale * sh, ch);
+    }
+    T s, c;
+    sincos_t(th, &s, &c);
+    const T d = (kind == MOT_PRISM) ? scale * qv : T(0);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const T a = f.r[3 * i], b = f.r[3 * i + 1];
+        f.r[3 * i] = fma(a, c, b * s);
+        f.r[3 * i + 1] = fma(b, c, -(a * s));
+        f.t[i] = fma(f.r[3 * i + 2], d, f.t[i]);
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void base_frame(Fr<T>& f, T bx, T by, T th) {  // src/transform.jl:33-37
+    set_identity(f);
+    T s, c;
+    sincos_t(th, &s, &c);
+    f.r[0] = c; f.r[1] = -s;
+    f.r[3] = s; f.r[4] = c;
+    f.t[0] = bx; f.t[1] = by;
+}
+
+// Output sink: runs of consecutive SoA rows of one array (a pose = 12 rows, a
+// Jacobian column = 6 or 3 rows) for this lane's configuration, one 4/8-byte
+// store per row.  (A 16-byte-per-lane variant staged through LDS measured 5%
+// slower: this stream runs at the ceiling of its access pattern, see
+// profiles/r01_store_probe.txt.)
+template <typename T>
+struct Sink {
+    uint32_t off;  // lane byte offset
+
+    template <int NR>
+    __device__ __forceinline__ void rows(T* __restrict__ base, int64_t row0, int64_t ld, const T (&v)[NR],
+                                         int nvalid) const {
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+            if (k < nvalid) st_soa(base, row0 + k, ld, off, v[k]);
+    }
+};
+
+// 3x4 column-major pose (k = row + 3*col) of output `o`: rows o*12 .. o*12+11
+template <typename T>
+__device__ __forceinline__ void store_pose(const Sink<T>& sk, T* __restrict__ poses, int64_t o, int64_t ld,
+                                           const Fr<T>& L) {
+    const T v[12] = {L.r[0], L.r[3], L.r[6], L.r[1], L.r[4], L.r[7], L.r[2], L.r[5], L.r[8], L.t[0], L.t[1], L.t[2]};
+    sk.rows(poses, o * 12, ld, v, 12);
+}
+
+template <typename T>
+__device__ __forceinline__ void link_frame(Fr<T>& L, const Fr<T>& C, bool has_x, const T* __restrict__ X) {
+    if (has_x) {
+        T Xr[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Xr[k] = X[k];
+        mul_rigid_regs(L, C, Xr);
+    } else {
+        L = C;
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ void slot_store(T* slots, int slot, int B, int tid, const Fr<T>& f) {
+    T* s = slots + (size_t)slot * 12 * B + tid;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s[k * B] = f.r[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s[(9 + k) * B] = f.t[k];
+}
+
+template <typename T>
+__device__ __forceinline__ void slot_load(const T* slots, int slot, int B, int tid, Fr<T>& f) {
+    const T* s = slots + (size_t)slot * 12 * B + tid;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f.r[k] = s[k * B];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.t[k] = s[(9 + k) * B];
+}
+
+// One phase-A step: C <- C F; record (o, z); motion.  Straight-line: padded
+// steps are identities with scale 0, so records and motion need no branch.
+template <typename T>
+__device__ __forceinline__ void step_a(Fr<T>& f, const KStep<T>& st, T qv, T (&o)[3], T (&z)[3]) {
+    mul_rigid(f, st.F);
+    o[0] = f.t[0]; o[1] = f.t[1]; o[2] = f.t[2];  // _get_joint_axis, src/algorithm.jl:42-54
+    const T sc = st.scale;
+    z[0] = f.r[2] * sc; z[1] = f.r[5] * sc; z[2] = f.r[8] * sc;
+    motion(f, st.kind, st.flags, sc, qv);
+}
+
+// One get_jacobian! column (src/algorithm.jl:65-81): revolute -> [z x (p - o); z or
+// rpy_derivative!(z)], prismatic -> [z; untouched (zeros with get_jacobian)].
+// Written to every column in the step's colmask.
+template <typename T>
+struct JacCtx {
+    T* jac;
+    int64_t ldj;
+    const Sink<T>* sink;
+    int rows;
+    bool with_rot, zero, rpy;
+    T px, py, pz;
+    T k11, k12, k21, k22, k31, k32;  // rpy_derivative! coefficients
+};
+
+template <typename T>
+__device__ __forceinline__ void emit_jcol(const JacCtx<T>& J, const KStep<T>& st, T ox, T oy, T oz, T zx, T zy,
+                                          T zz) {
+    T lin[3], ang[3];
+    const bool prism = st.jkind == MOT_PRISM;
+    if (prism) {
+        lin[0] = zx; lin[1] = zy; lin[2] = zz;
+        ang[0] = ang[1] = ang[2] = T(0);
+    } else {
+        const T dx = J.px - ox, dy = J.py - oy, dz = J.pz - oz;
+        lin[0] = fma(zy, dz, -(zz * dy));
+        lin[1] = fma(zz, dx, -(zx * dz));
+        lin[2] = fma(zx, dy, -(zy * dx));
+        if (J.rpy) {
+            ang[0] = fma(J.k11, zx, J.k12 * zy);
+            ang[1] = fma(J.k21, zx, J.k22 * zy);
+            ang[2] = fma(J.k31, zx, fma(J.k32, zy, zz));
+        } else {
+            ang[0] = zx; ang[1] = zy; ang[2] = zz;
+        }
+    }
+    const T v[6] = {lin[0], lin[1], lin[2], ang[0], ang[1], ang[2]};
+    const int nv = (J.with_rot && (!prism || J.zero)) ? 6 : 3;
+    uint64_t m = st.colmask;
+    while (m) {
+        const int c = __builtin_ctzll(m);
+        m &= m - 1;
+        J.sink->rows(J.jac, (int64_t)c * J.rows, J.ldj, v, nv);
+    }
+}
+
+// Block -> configuration chunk.  Workgroups are dispatched round-robin over the
+// 8 XCDs (block b on XCD b % 8); with KINHIP_XCD_REMAP each XCD instead takes
+// one contiguous eighth of the batch, so its L2 and DRAM pages see sequential
+// row segments rather than every eighth 1 KB piece.
+#ifndef KINHIP_XCD_REMAP
+#define KINHIP_XCD_REMAP 0
+#endif
+__device__ __forceinline__ uint32_t config_block() {
+#if KINHIP_XCD_REMAP
+    const uint32_t nb = gridDim.x, b = blockIdx.x, x = b & 7u, q = nb >> 3, r = nb & 7u;
+    return x * q + (x < r ? x : r) + (b >> 3);
+#else
+    return blockIdx.x;
+#endif
+}
+
+inline unsigned grid_of(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// phase-A sizes compiled (the stager pads the chain to one of these: pick_chain_bound)
+#define KIN_MAXA_DISPATCH(M, CALL) \
+    switch (M) {                   \
+    case 4: CALL(4); break;        \
+    case 8: CALL(8); break;        \
+    case 12: CALL(12); break;      \
+    case 16: CALL(16); break;      \
+    default: CALL(32); break;      \
+    }
+
+// Launches are split into chunks of kChunk configurations so that every lane
+// byte offset (uint32, ld_soa / st_soa) fits in 32 bits; chunks are pointer
+// offsets into the same SoA arrays (the leading dimensions do not change).
+constexpr int64_t kChunk = int64_t(1) << 27;
+
+}  // namespace kinhip

@@ -6,7 +6,7 @@
 
 namespace kinhip {
 
-// phase-A chain bounds compiled into the kernels (kinhip_kernels.hip)
+// phase-A chain bounds compiled into the kernels (kinhip_device.h KIN_MAXA_DISPATCH)
 inline int pick_chain_bound(int n) { return n <= 4 ? 4 : n <= 8 ? 8 : n <= 12 ? 12 : n <= 16 ? 16 : 32; }
 
 struct LaunchGeom {

@@ -1,5 +1,5 @@
 // kinhip_prog.h -- staged evaluation program shared by the host stager
-// (kinhip_host.cpp) and the gfx950 kernels (kinhip_kernels.hip).
+// (kinhip_host.cpp) and the gfx950 kernels (kinhip_fk.hip, kinhip_ik.hip, kinhip_coll.hip).
 //
 // A plan compiles the reference's per-link transform chain
 // (src/algorithm.jl:6-37 + joint_transform, src/mechanism.jl:90-103) into a

@@ -4,9 +4,11 @@ import re
 import sys
 from collections import Counter
 
-S = "kinematics.jl_amd/lib/obj/kinhip_kernels.s"
+import glob
 pat = sys.argv[1]
-lines = open(S).read().split("\n")
+lines = []
+for S in sorted(glob.glob("kinematics.jl_amd/lib/obj/kinhip_*.s")):
+    lines += open(S).read().split("\n")
 start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*:", l) and pat in l)
 end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
 body = [l.split(";")[0].strip() for l in lines[start:end]]
