@@ -20,17 +20,24 @@ template <typename T>
 __device__ __forceinline__ T box_key(T qx, T qy, T qz) {
     const T mx = fmax(qx, fmax(qy, qz));
     const T ox = fmax(qx, T(0)), oy = fmax(qy, T(0)), oz = fmax(qz, T(0));
-    const T oo = fma(ox, ox, fma(oy, oy, oz * oz));
-    return mx > T(0) ? oo : -(mx * mx);
+    const T mn = fmin(mx, T(0));  // 0 outside, max(q) inside (where every o is 0)
+    return fma(ox, ox, fma(oy, oy, fma(oz, oz, -(mn * mn))));
 }
 
+// d from its surrogate d|d|: one square root (hardware v_sqrt_f32 for fp32, <= 1 ulp)
+__device__ __forceinline__ float signed_sqrt(float k) { return copysignf(__builtin_amdgcn_sqrtf(fabsf(k)), k); }
+__device__ __forceinline__ double signed_sqrt(double k) { return copysign(sqrt(fabs(k)), k); }
+
+#ifndef KINHIP_AABB_UNROLL
+#define KINHIP_AABB_UNROLL 2
+#endif
 template <typename T, bool GRAD>
 __device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
                                        int nb, T px, T py, T pz, T (&gw)[3]) {
     T best = T(INFINITY);
     int bk = 0;
     // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
-#pragma clang loop vectorize(disable) unroll_count(2)
+#pragma clang loop vectorize(disable) unroll_count(KINHIP_AABB_UNROLL)
     for (int k = 0; k < na; ++k) {  // axis-aligned boxes: no rotation
         const KAabb<T>& b = aabb[k];
         const T key = box_key(fabs(px - b.c[0]) - b.half[0], fabs(py - b.c[1]) - b.half[1],
@@ -60,7 +67,7 @@ __device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const 
             best = fmin(best, key);
         }
     }
-    const T d = best > T(0) ? sqrt_t(best) : -sqrt_t(-best);
+    const T d = signed_sqrt(best);
     if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
         const KBox<T>& b = boxes[bk];
         T l[3], q[3], gl[3];

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib as K
-from .mechanism import Link, Mechanism, _device, _i32, _p, get_transform
+from .mechanism import Link, Mechanism, _device, _i32, _ld_of, _p, get_transform
 
 _DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
 _uid = itertools.count()
@@ -111,18 +111,23 @@ class CollisionPlan:
 
     def run(self, sdf: UnionSDF, Q: torch.Tensor, dists=True, grads=False, min_dist=False,
             truncation=float("inf"), stream=None):
-        """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async."""
+        """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async.
+        `dists` / `grads` may also be preallocated (row-padded) output views of those shapes."""
         if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
         N = Q.shape[1]
         dev = Q.device
-        D = torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None
-        G = torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None
+        D = dists if isinstance(dists, torch.Tensor) else (
+            torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None)
+        G = grads if isinstance(grads, torch.Tensor) else (
+            torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None)
         Mn = torch.empty(N, dtype=self.dtype, device=dev) if min_dist else None
+        ldd = _ld_of(D.unsqueeze(0), (1, self.n_sph, N), self.dtype) if D is not None else N
+        ldg = _ld_of(G, (self.n_sph, self.n_dof, N), self.dtype) if G is not None else N
         st = (stream or torch.cuda.current_stream(dev)).cuda_stream
         ptr = lambda t: t.data_ptr() if t is not None else None
-        K.check(K.lib().kin_coll_batch(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0), N, ptr(D), N,
-                                       ptr(G), N, ptr(Mn), st))
+        K.check(K.lib().kin_coll_batch(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0), N, ptr(D), ldd,
+                                       ptr(G), ldg, ptr(Mn), st))
         return D, G, Mn
 
 

@@ -191,3 +191,48 @@ def test_gpu_collision_box_kinds(dtype):
     np.testing.assert_allclose(Mn.double().cpu().numpy(), rd.min(0), atol=tol)
     bad = np.abs(G.double().cpu().numpy() - rgr) > (2e-5 if dtype == torch.float64 else 1e-4)
     assert bad.mean() < 1e-3, bad.mean()
+
+
+@pytest.mark.gpu
+def test_gpu_collision_edges_and_errors():
+    """Empty / single / ragged batches, a scene of many random boxes, and the error paths."""
+    import kinhip
+    from kinhip._lib import KinError
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    rng = np.random.default_rng(12)
+    poses, widths = [], []
+    for _ in range(300):
+        R = O.rpy_to_matrix(rng.uniform(-np.pi, np.pi, 3)) if rng.random() < 0.5 else np.eye(3)
+        poses.append(_T(rng.uniform([-1, -1, 0], [1.5, 1, 1.5]), R))
+        widths.append(rng.uniform(0.02, 0.3, 3))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    plan = sscc.plan(arm, dtype=torch.float64)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    box = O.OracleUnionSDF(poses, widths)
+    ids = [tree.joint_id(n) for n in ARM]
+    for N in (1, 65, 1000):
+        Q = torch.tensor(rng.uniform(-1.2, 1.2, (8, N)), dtype=torch.float64, device=dev)
+        D, G, Mn = plan.run(sdf, Q, grads=True, min_dist=True)
+        rd, rg = O.coll_batch(om, box, Q.cpu().numpy(), ids, sph, rad)
+        np.testing.assert_allclose(D.cpu().numpy(), rd, atol=1e-9)
+        np.testing.assert_allclose(Mn.cpu().numpy(), rd.min(0), atol=1e-9)
+        assert (np.abs(G.cpu().numpy() - rg) > 2e-5).mean() < 1e-3
+    D, G, Mn = plan.run(sdf, torch.zeros((8, 0), dtype=torch.float64, device=dev), grads=True, min_dist=True)
+    assert D.shape == (len(sph), 0) and Mn.shape == (0,)
+    # error paths
+    fk_plan = m.plan(arm, out_links=[m.find_link("gripper_link")], dtype=torch.float64)
+    Q = torch.zeros((8, 4), dtype=torch.float64, device=dev)
+    with pytest.raises(KinError):
+        kinhip._lib.check(kinhip._lib.lib().kin_coll_batch(fk_plan._h, sdf._h, 1.0, Q.data_ptr(), 4, 4, None, 4,
+                                                           None, 4, None, None))
+    with pytest.raises(KinError):
+        kinhip._lib.check(kinhip._lib.lib().kin_ineq_const_batch(plan._h, sdf._h, float("inf"), Q.data_ptr(), 4, 4,
+                                                                 Q.data_ptr(), 4, None, 4, None))
+    with pytest.raises(ValueError):
+        kinhip.UnionSDF([])
+    # a sphere on another branch than the batch chain (head) is outside the engine's limits
+    m2, sscc2, arm2 = _gpu_setup(False)
+    sscc2.add_coll_sphere(m2.find_link("head_pan_link"), (0.0, 0.0, 0.1), 0.1)
+    with pytest.raises(KinError):
+        sscc2.plan(arm2 + [m2.find_joint("head_pan_joint")], dtype=torch.float64)

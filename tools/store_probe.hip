@@ -8,17 +8,18 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e)); return 1; } } while (0)
 
 // P1: one config per lane, read 8 rows, write R rows (4 B per lane per row)
+// rows `ld` elements apart (ld = n: dense; ld = n + 256: the bench's padded rows)
 template <bool NT>
-__global__ void p_narrow(const float* __restrict__ q, float* __restrict__ out, long n, int R) {
+__global__ void p_narrow(const float* __restrict__ q, float* __restrict__ out, long n, int R, long ld) {
     long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float a = 0;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) a += q[r * n + i];
+    for (int r = 0; r < 8; ++r) a += q[r * ld + i];
     for (int r = 0; r < R; ++r) {
         float v = a + r;
-        if (NT) __builtin_nontemporal_store(v, out + (long)r * n + i);
-        else out[(long)r * n + i] = v;
+        if (NT) __builtin_nontemporal_store(v, out + (long)r * ld + i);
+        else out[(long)r * ld + i] = v;
     }
 }
 // P2: four consecutive configs per lane (16 B per lane per row, 1 KB per row per wave)
@@ -48,9 +49,12 @@ int main() {
     const long n = 1 << 20;
     const int R = 60;
     float *q, *out;
-    CK(hipMalloc(&q, 8 * n * 4));
-    CK(hipMalloc(&out, (long)R * n * 4));
-    CK(hipMemset(q, 0, 8 * n * 4));
+    const long ldp = n + 256;
+    CK(hipMalloc(&q, 8 * ldp * 4));
+    CK(hipMalloc(&out, (long)R * ldp * 4));
+    CK(hipMemset(q, 0, 8 * ldp * 4));
+    float* out2;
+    CK(hipMalloc(&out2, 126L * n * 4));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -69,10 +73,14 @@ int main() {
     };
     const double bytes = (8.0 + R) * n * 4;
     for (int rep = 0; rep < 2; ++rep) {
-        timeit("narrow_60rows_plain", bytes, [&] { p_narrow<false><<<n / 256, 256>>>(q, out, n, R); });
-        timeit("narrow_60rows_nt", bytes, [&] { p_narrow<true><<<n / 256, 256>>>(q, out, n, R); });
+        timeit("narrow_60rows_plain", bytes, [&] { p_narrow<false><<<n / 256, 256>>>(q, out, n, R, n); });
+        timeit("narrow_60rows_nt", bytes, [&] { p_narrow<true><<<n / 256, 256>>>(q, out, n, R, n); });
+        timeit("narrow_60rows_plain_pad256", bytes, [&] { p_narrow<false><<<n / 256, 256>>>(q, out, n, R, ldp); });
+        timeit("narrow_60rows_nt_pad256", bytes, [&] { p_narrow<true><<<n / 256, 256>>>(q, out, n, R, ldp); });
         timeit("vec4_60rows_plain", bytes, [&] { p_vec4<false><<<n / 4 / 256, 256>>>((float4*)q, (float4*)out, n / 4, R); });
         timeit("vec4_60rows_nt", bytes, [&] { p_vec4<true><<<n / 4 / 256, 256>>>((float4*)q, (float4*)out, n / 4, R); });
+        timeit("narrow_126rows_nt (config-5 grads: 8 in, 14 + 112 out)", (8.0 + 126) * n * 4,
+               [&] { p_narrow<true><<<n / 256, 256>>>(q, out2, n, 126, n); });
         timeit("fill_contig_60n", (double)R * n * 4, [&] { p_fill<<<R * n / 4 / 256, 256>>>((float4*)out, R * n / 4); });
     }
     return 0;
