@@ -246,7 +246,7 @@ def main():
     lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
     stream = torch.cuda.Stream(dev)
 
-    def leg(dtype, jac, links, n=N, pad=args.row_pad):
+    def leg(dtype, jac, links, n=N, pad=args.row_pad, start=None):
         """Device-resident SoA buffers; every row padded to ld = n + pad elements (the C-ABI's
         ldq / ldp / ldj): rows exactly 2^k elements apart line all 68 streams of a wave up on the
         same HBM channels (tools/ld_probe.py, profiles/r01_row_pad_probe.txt)."""
@@ -254,7 +254,8 @@ def main():
                       with_rot=True, dtype=dtype)
         ld = n + pad
         Qb = torch.empty((8, ld), dtype=dtype, device=dev)
-        Qb[:, :n] = kinhip.uniform_configs(lo, hi, n, start=rank * n, dtype=dtype, device=dev)
+        Qb[:, :n] = kinhip.uniform_configs(lo, hi, n, start=rank * n if start is None else start, dtype=dtype,
+                                           device=dev)
         poses = torch.empty((len(links), 12, ld), dtype=dtype, device=dev)[:, :, :n]
         J = torch.empty((8, 6, ld), dtype=dtype, device=dev)[:, :, :n] if jac else None
         return plan, Qb[:, :n], poses, J
@@ -298,16 +299,13 @@ def main():
                                           "achieved_GBs": bytes_per_eval * n_s / (ds_ / k_s) / 1e9}
                 del ps, Qs, Ps, Js
         out["batch_sweep_fk_jac_f32"] = sweep
-        if ws > 1:  # strong scaling: one global 2^20 batch split across the ranks
-            st0, cnt = D.split_range(N, rank, ws)
-            ps = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
-            Qs = kinhip.uniform_configs(lo, hi, cnt, start=st0, dtype=torch.float32, device=dev)
-            Ps = torch.empty((1, 12, cnt), dtype=torch.float32, device=dev)
-            Js = torch.empty((8, 6, cnt), dtype=torch.float32, device=dev)
-            w_s, d_s = _time_plan(ps, Qs, Ps, Js, args.steps, args.warmup, ctx, stream)
-            out["strong_scaling_fk_jac_f32"] = {"global_batch": N, "value": N * args.steps / w_s, "unit": "evals/s",
-                                                "ms_per_step": w_s / args.steps * 1e3}
-            del ps, Qs, Ps, Js
+    if ws > 1:  # strong scaling: one global 2^20 batch split across the ranks
+        st0, cnt = D.split_range(N, rank, ws)
+        ps, Qs, Ps, Js = leg(torch.float32, True, [gl], n=cnt, start=st0)
+        w_s, d_s = _time_plan(ps, Qs, Ps, Js, args.steps, args.warmup, ctx, stream)
+        out["strong_scaling_fk_jac_f32"] = {"global_batch": N, "value": N * args.steps / w_s, "unit": "evals/s",
+                                            "ms_per_step": w_s / args.steps * 1e3}
+        del ps, Qs, Ps, Js
     if args.extras:
         # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
         p64, Q64, P64, J64 = leg(torch.float64, True, [gl])
