@@ -205,7 +205,10 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
                                     offs, ro, rz, bx, by, off,
                               dists, ldd, grads, ldg, dmin);
     }
-    if (min_dist) st_soa(min_dist, 0, 0, off, dmin);
+    if (min_dist) {
+        if (a.accumulate) dmin = fmin(dmin, ld_soa(min_dist, 0, 0, off));
+        st_soa(min_dist, 0, 0, off, dmin);
+    }
 }
 
 }  // namespace

@@ -186,6 +186,8 @@ struct kin_plan {
     bool is_coll = false;
     int32_t n_sph = 0;
     void* d_sph = nullptr;
+    // spheres on several chains: one staged program per chain (kin_coll_plan_create)
+    std::vector<std::unique_ptr<kin_plan>> parts;
     ~kin_plan() {
         if (d_steps) (void)hipFree(d_steps);
         if (d_sph) (void)hipFree(d_sph);
@@ -283,6 +285,7 @@ struct Stager {
     std::vector<int32_t> chain, chain_step;  // phase-A nodes root..spine and their edge steps (-1: none)
     // collision plans
     const kin_coll_desc* coll = nullptr;
+    const int32_t* sph_out = nullptr;  // global sphere index of each desc sphere (multi-chain plans)
     std::vector<SphD> spheres;
     int32_t sph_root0 = 0, sph_root1 = 0;
     // LDS slots
@@ -423,7 +426,7 @@ struct Stager {
             const double c2 = coll->centers ? coll->centers[3 * k + 2] : 0.0;
             for (int i = 0; i < 3; ++i) sd.c[i] = S.r[3 * i] * c0 + S.r[3 * i + 1] * c1 + S.r[3 * i + 2] * c2 + S.t[i];
             sd.r = coll->radii[k];
-            sd.out = k;
+            sd.out = sph_out ? sph_out[k] : k;
             sd.step = (x == sroot) ? -1 : chain_step[on_chain[x]];
             if (x != sroot && sd.step < 0) return set_error(KIN_E_INVALID, "coll plan: internal (no step)");
             spheres.push_back(sd);
@@ -1054,28 +1057,89 @@ int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** 
         if (j < 0 || j >= J) return set_error(KIN_E_KEY, "kin_coll_plan_create: q joint id out of range");
         moving[j] = m->jtype[j] != KIN_JOINT_FIXED;
     }
-    // spine: the sphere anchor (nearest link below a moving joint) with the most moving joints above it
-    int32_t spine = -1, best = -1;
+    // Group the spheres by chain: the spine of a group is the remaining sphere anchor (nearest link
+    // below a moving joint) with the most moving joints above it; the group takes every remaining
+    // sphere whose anchor lies on the spine's root path.  One staged program per group.
+    std::vector<int32_t> anchor(c->n_spheres), depth(c->n_spheres);
     for (int32_t k = 0; k < c->n_spheres; ++k) {
         int32_t x = c->sphere_link_ids[k] - 1;
         if (x < 0 || x >= L) return set_error(KIN_E_KEY, "kin_coll_plan_create: sphere link id out of range");
         while (x >= 0 && m->link_pjoint[x] >= 0 && !moving[m->link_pjoint[x]]) x = m->plink(x);
-        int depth = 0;
-        for (int32_t y = x; y >= 0 && m->link_pjoint[y] >= 0; y = m->plink(y)) depth += moving[m->link_pjoint[y]];
-        if (depth > best) {
-            best = depth;
-            spine = x;
-        }
+        int dd = 0;
+        for (int32_t y = x; y >= 0 && m->link_pjoint[y] >= 0; y = m->plink(y)) dd += moving[m->link_pjoint[y]];
+        anchor[k] = x;
+        depth[k] = dd;
     }
-    kin_plan_desc d{c->dtype, c->n_q, c->q_joint_ids, 0, nullptr, spine + 1, c->n_q, c->q_joint_ids, 0};
-    auto P = std::make_unique<kin_plan>();
-    Stager st(*m, d);
-    st.coll = c;
-    const int rc = st.run(*P);
-    if (rc != KIN_OK) return rc;
-    *out = P.release();
+    std::vector<char> done(c->n_spheres, 0);
+    std::vector<std::unique_ptr<kin_plan>> parts;
+    int32_t left = c->n_spheres;
+    while (left > 0) {
+        int32_t spine = -1, best = -1;
+        for (int32_t k = 0; k < c->n_spheres; ++k)
+            if (!done[k] && depth[k] > best) { best = depth[k]; spine = anchor[k]; }
+        std::vector<char> on_path(L, 0);
+        for (int32_t y = spine; y >= 0; y = m->plink(y)) on_path[y] = 1;
+        std::vector<int32_t> ids, outs;
+        std::vector<double> cen, rad;
+        for (int32_t k = 0; k < c->n_spheres; ++k) {
+            if (done[k] || !on_path[anchor[k]]) continue;
+            done[k] = 1;
+            --left;
+            ids.push_back(c->sphere_link_ids[k]);
+            outs.push_back(k);
+            rad.push_back(c->radii[k]);
+            for (int i = 0; i < 3; ++i) cen.push_back(c->centers ? c->centers[3 * k + i] : 0.0);
+        }
+        kin_coll_desc sub{c->dtype, c->n_q, c->q_joint_ids, (int32_t)ids.size(), ids.data(), cen.data(), rad.data()};
+        kin_plan_desc d{c->dtype, c->n_q, c->q_joint_ids, 0, nullptr, spine + 1, c->n_q, c->q_joint_ids, 0};
+        auto P = std::make_unique<kin_plan>();
+        Stager st(*m, d);
+        st.coll = &sub;
+        st.sph_out = outs.data();
+        const int rc = st.run(*P);
+        if (rc != KIN_OK) return rc;
+        parts.push_back(std::move(P));
+    }
+    std::unique_ptr<kin_plan> top;
+    if (parts.size() == 1) {
+        top = std::move(parts[0]);
+    } else {
+        top = std::make_unique<kin_plan>();
+        top->dtype = parts[0]->dtype;
+        top->nqcols = parts[0]->nqcols;
+        top->with_base = parts[0]->with_base;
+        top->n_q = parts[0]->n_q;
+        top->is_coll = true;
+        top->n_sph = c->n_spheres;
+        top->parts = std::move(parts);
+    }
+    top->n_sph = c->n_spheres;
+    *out = top.release();
     return KIN_OK;
 }
+
+namespace {
+// k_coll over every chain program of a collision plan; min_dist accumulates after the first
+int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q, int64_t ldq, int64_t n, void* dists,
+                int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream) {
+    const size_t np = p->parts.empty() ? 1 : p->parts.size();
+    for (size_t k = 0; k < np; ++k) {
+        const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
+        a.accumulate = k > 0;
+        hipError_t e;
+        if (s->dtype == KIN_F32)
+            e = launch_coll<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
+                                   (const KBox<float>*)sdf->d_f32, s->geom, a, (const float*)q, ldq, n, (float*)dists,
+                                   ldd, (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
+        else
+            e = launch_coll<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
+                                    (const KBox<double>*)sdf->d_f64, s->geom, a, (const double*)q, ldq, n,
+                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, (hipStream_t)stream);
+        if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
+    }
+    return KIN_OK;
+}
+}  // namespace
 
 int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq, int64_t n,
                    void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream) {
@@ -1085,18 +1149,8 @@ int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, con
     if (n == 0) return KIN_OK;
     if ((p->nqcols > 0 && (!q || ldq < n)) || (dists && ldd < n) || (grads && ldg < n))
         return set_error(KIN_E_INVALID, "kin_coll_batch: bad pointer / stride");
-    CollArgs a{truncation, 0.0, sdf->n_boxes, sdf->n_aabb};
-    hipError_t e;
-    if (p->dtype == KIN_F32)
-        e = launch_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
-                               (const KBox<float>*)sdf->d_f32, p->geom, a, (const float*)q, ldq, n, (float*)dists, ldd,
-                               (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
-    else
-        e = launch_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
-                                (const KBox<double>*)sdf->d_f64, p->geom, a, (const double*)q, ldq, n, (double*)dists,
-                                ldd, (double*)grads, ldg, (double*)min_dist, (hipStream_t)stream);
-    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
-    return KIN_OK;
+    CollArgs a{truncation, 0.0, sdf->n_boxes, sdf->n_aabb, 0};
+    return coll_launch(p, sdf, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, stream);
 }
 
 int kin_ineq_const_batch(const kin_plan* p, const kin_sdf* sdf, double margin, const void* q, int64_t ldq, int64_t n,
@@ -1109,18 +1163,8 @@ int kin_ineq_const_batch(const kin_plan* p, const kin_sdf* sdf, double margin, c
     if ((p->nqcols > 0 && (!q || ldq < n)) || !vals || ldv < n || (jac && ldj < n))
         return set_error(KIN_E_INVALID, "kin_ineq_const_batch: bad pointer / stride");
     // src/planning.jl:56, :66: truncation_dist = margin + 0.05; val = dist - margin
-    CollArgs a{margin + 0.05, margin, sdf->n_boxes, sdf->n_aabb};
-    hipError_t e;
-    if (p->dtype == KIN_F32)
-        e = launch_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
-                               (const KBox<float>*)sdf->d_f32, p->geom, a, (const float*)q, ldq, n, (float*)vals, ldv,
-                               (float*)jac, ldj, nullptr, (hipStream_t)stream);
-    else
-        e = launch_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
-                                (const KBox<double>*)sdf->d_f64, p->geom, a, (const double*)q, ldq, n, (double*)vals,
-                                ldv, (double*)jac, ldj, nullptr, (hipStream_t)stream);
-    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
-    return KIN_OK;
+    CollArgs a{margin + 0.05, margin, sdf->n_boxes, sdf->n_aabb, 0};
+    return coll_launch(p, sdf, a, q, ldq, n, vals, ldv, jac, ldj, nullptr, stream);
 }
 
 int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, const void* q, int64_t ldq, int64_t n,

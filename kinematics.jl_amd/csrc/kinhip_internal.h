@@ -42,6 +42,7 @@ struct CollArgs {
     double offset;    // subtracted from every reported distance (IneqConst margin)
     int32_t n_boxes;  // KBox array (sorted: the first n_aabb are axis-aligned)
     int32_t n_aabb;   // KAabb array placed right after the KBox array
+    int32_t accumulate;  // min_dist = min(min_dist, this launch's minimum) (multi-chain plans)
 };
 
 template <typename T>

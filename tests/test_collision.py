@@ -231,8 +231,38 @@ def test_gpu_collision_edges_and_errors():
                                                                  Q.data_ptr(), 4, None, 4, None))
     with pytest.raises(ValueError):
         kinhip.UnionSDF([])
-    # a sphere on another branch than the batch chain (head) is outside the engine's limits
-    m2, sscc2, arm2 = _gpu_setup(False)
-    sscc2.add_coll_sphere(m2.find_link("head_pan_link"), (0.0, 0.0, 0.1), 0.1)
-    with pytest.raises(KinError):
-        sscc2.plan(arm2 + [m2.find_joint("head_pan_joint")], dtype=torch.float64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gpu_collision_multi_chain(dtype):
+    """Spheres on two moving chains (arm + head pan/tilt as batch joints): one staged program per
+    chain, min distance accumulated across them, gradient columns of the other chain zero."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    sscc.add_coll_sphere(m.find_link("head_pan_link"), (0.05, 0.0, 0.1), 0.12)
+    sscc.add_coll_sphere(m.find_link("head_tilt_link"), (0.1, 0.0, 0.0), 0.1)
+    joints = arm + [m.find_joint("head_pan_joint"), m.find_joint("head_tilt_joint")]
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=(1.2, 0.0, 0.0))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    plan = sscc.plan(joints, dtype=dtype)
+    N = 1500
+    g = torch.Generator().manual_seed(21)
+    Q = (torch.rand((10, N), generator=g, dtype=torch.float64) * 2 - 1).to(dtype).to(dev)
+    D, G, Mn = plan.run(sdf, Q, grads=True, min_dist=True)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    sph.append(om.add_new_link(tree.link_id("head_pan_link"), _T((0.05, 0.0, 0.1))))
+    sph.append(om.add_new_link(tree.link_id("head_tilt_link"), _T((0.1, 0.0, 0.0))))
+    rad += [0.12, 0.1]
+    ids = [tree.joint_id(n) for n in ARM] + [tree.joint_id("head_pan_joint"), tree.joint_id("head_tilt_joint")]
+    rd, rg = O.coll_batch(om, O.OracleUnionSDF(poses, widths), Q.double().cpu().numpy(), ids, sph, rad)
+    tol = 1e-9 if dtype == torch.float64 else 2e-5
+    np.testing.assert_allclose(D.double().cpu().numpy(), rd, atol=tol)
+    np.testing.assert_allclose(Mn.double().cpu().numpy(), rd.min(0), atol=tol)
+    gd = G.double().cpu().numpy()
+    assert (np.abs(gd - rg) > (2e-5 if dtype == torch.float64 else 1e-4)).mean() < 1e-3
+    assert not np.any(gd[:14, 8:]) and not np.any(gd[14:, 1:8])  # arm spheres vs head joints and vice versa
+    V, Jv = kinhip.IneqConst(sscc, joints, sdf, 1, 0.03, dtype=dtype).eval_batch(Q)
+    np.testing.assert_allclose(V.double().cpu().numpy(), np.minimum(rd, 0.08) - 0.03, atol=tol)
