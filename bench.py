@@ -154,6 +154,34 @@ def _coll_leg(ctx, stream, n, steps):
     return out
 
 
+def _nakamura_leg(m, arm, gl, ctx, stream, n=1 << 18, reps=5):
+    """point_inverse_kinematics_nakamura (50 SR-inverse iterations, the reference's
+    `.+ 1.0` quirk), fp64 as the reference, `n` reachable points per GPU from q0 = 0."""
+    dt = torch.float64
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, jac_joints=arm, with_rot=False, dtype=dt)
+    start, cnt = D.shard_range(n, ctx.rank)
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], cnt, start=start,
+                                seed=99, dtype=dt, device=ctx.device)
+    pts = plan.run(Qt)[0][0][9:12].contiguous()
+    Qs = [torch.zeros((8, cnt), dtype=dt, device=ctx.device) for _ in range(reps + 1)]
+    with torch.cuda.stream(stream):
+        plan.point_ik_nakamura(pts, Qs[0], stream=stream)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        for k in range(1, reps + 1):
+            plan.point_ik_nakamura(pts, Qs[k], stream=stream)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    wall = D.max_over_ranks(ctx, [time.perf_counter() - t0])[0]
+    got = plan.run(Qs[-1])[0][0][9:12]
+    err = (got - pts).norm(dim=0)
+    return {"value": n * ctx.world * reps / wall, "unit": "point-IK solves/s (50 iterations each)",
+            "points_per_gpu": n, "ms_per_batch": wall / reps * 1e3, "dtype": "f64",
+            "median_residual_m": float(err.median())}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -323,6 +351,7 @@ def main():
         del p2, Q2, P2
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))
+        out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream)
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = _cpu_baseline(m)
     if rank == 0:
