@@ -111,3 +111,55 @@ def test_gpu_random_tree_vs_oracle(tmp_path, seed):
         if dtype == torch.float32:  # sentinel was rounded to fp32 on the device
             rj = np.where(rj == init, init.astype(np.float32).astype(np.float64), rj)
         np.testing.assert_allclose(got, rj, atol=tol, rtol=1e-4 if dtype == torch.float32 else 1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", SEEDS[:24])
+def test_gpu_random_tree_collision_vs_oracle(tmp_path, seed):
+    """Spheres on random links of random trees (often several moving chains -> multi-program plans)
+    against random boxes: distances, min distance and gradients vs the oracle (fp64)."""
+    import kinhip
+    from kinhip._lib import KinError, KIN_E_UNSUPPORTED
+    rng = np.random.default_rng(5000 + seed)
+    p = _write(str(tmp_path), random_urdf(rng, int(rng.integers(3, 30)), chain_bias=rng.uniform(0.4, 0.9)), seed)
+    t = O.parse_urdf_tree(p)
+    moving = [k + 1 for k in range(len(t.joint_names)) if t.joint_type[k] != 0]
+    if not moving:
+        pytest.skip("no moving joint")
+    with_base = bool(rng.random() < 0.4)
+    m = kinhip.parse_urdf(p, with_base=with_base)
+    om = O.OracleMech(t, with_base=with_base)
+    q_ids = [int(x) for x in rng.choice(moving, int(rng.integers(1, min(len(moving), 10) + 1)), replace=False)]
+    sscc = kinhip.SweptSphereCollisionChecker(m)
+    sph, rad = [], []
+    for _ in range(int(rng.integers(1, 10))):
+        lk = int(rng.integers(1, len(t.link_names) + 1))
+        c, r = rng.uniform(-0.1, 0.1, 3), float(rng.uniform(0.02, 0.1))
+        sscc.add_coll_sphere(m.links[lk - 1], c, r)
+        T = np.eye(4)
+        T[:3, 3] = c
+        sph.append(om.add_new_link(lk, T))
+        rad.append(r)
+    poses, widths = [], []
+    for _ in range(5):
+        T = np.eye(4)
+        if rng.random() < 0.5:
+            T[:3, :3] = O.rpy_to_matrix(rng.uniform(-np.pi, np.pi, 3))
+        T[:3, 3] = rng.uniform(-1, 1, 3)
+        poses.append(T)
+        widths.append(rng.uniform(0.05, 0.5, 3))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    try:
+        plan = sscc.plan([m.joints[j - 1] for j in q_ids], dtype=torch.float64)
+    except KinError as e:
+        if e.code == KIN_E_UNSUPPORTED:
+            pytest.skip(f"outside the engine limits: {e}")
+        raise
+    N = 300
+    Q = rng.uniform(-2, 2, (len(q_ids) + (3 if with_base else 0), N))
+    Qd = torch.tensor(Q, dtype=torch.float64, device="cuda")
+    D, G, Mn = plan.run(sdf, Qd, grads=True, min_dist=True)
+    rd, rg = O.coll_batch(om, O.OracleUnionSDF(poses, widths), Q, q_ids, sph, rad)
+    np.testing.assert_allclose(D.cpu().numpy(), rd, atol=1e-9)
+    np.testing.assert_allclose(Mn.cpu().numpy(), rd.min(0), atol=1e-9)
+    assert (np.abs(G.cpu().numpy() - rg) > 2e-5 * (1 + np.abs(rg))).mean() < 2e-3
