@@ -127,49 +127,95 @@ __device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S,
 #ifndef KINHIP_IK_WAVES
 #define KINHIP_IK_WAVES 1
 #endif
+// Work distribution: wave w owns targets [w*chunk, (w+1)*chunk) and keeps its
+// 64/G lane groups busy: a group whose target is finished (all its lanes done)
+// writes the result and takes the wave's next target at once, so a wave no
+// longer waits for its slowest target before the others move on.  The queue is
+// wave-local (ballot + popcount, no atomics, nothing in memory between launches).
 template <typename T, int MAXA, int ROWS, int G>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_WAVES))) void k_ik_dls(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                 const IkArgsT<T> a, const T* __restrict__ tgt, int64_t ldt,
                                                 T* __restrict__ q, int64_t ldq, int64_t n,
                                                 int32_t* __restrict__ iters, T* __restrict__ err,
-                                                int64_t lde) {
-    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t i = gt / G;  // target (lanes of one target are adjacent: same wave)
-    const int slot = (int)(gt % G);
-    const bool valid = i < (uint64_t)n;
-    const uint32_t off = (valid ? i : 0u) * (uint32_t)sizeof(T);
-    T Rt[9], pt[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-#pragma unroll
-        for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
-        pt[r] = ld_soa(tgt, 9 + r, ldt, off);
-    }
+                                                int64_t lde, int64_t chunk) {
+    const int lane = (int)(threadIdx.x & 63u);
+    const int slot = lane % G, grp = lane / G;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t wbeg = wave * chunk, wend = wbeg + chunk < n ? wbeg + chunk : n;
+    int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
+    int64_t i = 0;
+    bool have = false;    // the first pass of the loop hands every group its first target
     const bool base = (P.flags & PF_BASE) != 0;
-    T b0[3] = {T(0), T(0), T(0)};
-    if (base)
-        for (int k = 0; k < 3; ++k) b0[k] = ld_soa(q, P.base_col + k, ldq, off);
-    const int64_t gi = a.ibase + (int64_t)i;
     const int L = a.attempt_len;
+    const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << (grp * G));
 
-    int att = slot;
-    bool done = !valid || att >= a.n_attempts;
-    int res_att = INT_MAX;  // attempt at which this lane converged
-    bool final_lane = false;
-    T qs[MAXA], b[3] = {b0[0], b0[1], b0[2]};
-    int it = att > 0 ? att * L + 1 : 0;
-    ik_start_attempt<T, MAXA>(S, a, q, ldq, off, gi, att, qs);
+    T Rt[9], pt[3], b0[3], qs[MAXA], b[3];
+    int att = 0, it = 0, res_att = INT_MAX;
+    bool done = true, final_lane = false;
+    uint32_t off = 0;
     T ep = 0, er = 0;
+    auto start_target = [&]() {
+        off = (uint32_t)i * (uint32_t)sizeof(T);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
+            pt[r] = ld_soa(tgt, 9 + r, ldt, off);
+        }
+        b0[0] = b0[1] = b0[2] = T(0);
+        if (base)
+            for (int k = 0; k < 3; ++k) b0[k] = ld_soa(q, P.base_col + k, ldq, off);
+        b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
+        att = slot;
+        done = att >= a.n_attempts;
+        res_att = INT_MAX;
+        final_lane = false;
+        it = att > 0 ? att * L + 1 : 0;
+        ep = er = T(0);
+        ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
+    };
     T ro[MAXA][3], rz[MAXA][3];
     for (;;) {
-        if constexpr (G > 1) {  // lowest converged attempt of this target so far
-            int gm = res_att;
+        int gm = res_att;  // lowest converged attempt of this lane group's target so far
+        if constexpr (G > 1) {
 #pragma unroll
             for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
-            if (!done && gm < att) done = true;
+            if (have && !done && gm < att) done = true;
         }
-        if (__ballot(!done) == 0) break;  // wave-uniform exit: every lane finished or superseded
-        if (done) continue;
+        // a group whose lanes are all done writes its target and takes the next one
+        const uint64_t dmask = __ballot(!have || done);
+        const bool gfin = have && (dmask & gmask) == gmask;
+        if (gfin) {
+            const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
+            if (writer) {
+#pragma unroll
+                for (int s2 = 0; s2 < MAXA; ++s2) {
+                    const int32_t c = S[s2].qcol;
+                    if (c >= 0) st_soa(q, c, ldq, off, qs[s2]);
+                }
+                if (base)
+                    for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
+                if (iters) iters[i] = it;
+                if (err) {
+                    st_soa(err, 0, lde, off, ep);
+                    st_soa(err, 1, lde, off, er);
+                }
+            }
+            have = false;
+        }
+        const uint64_t need = __ballot(!have && slot == 0) & ~0ull;  // group leaders asking for work
+        if (need && next < wend) {
+            const uint64_t lead = 1ull << (grp * G);
+            const int rank = __popcll(need & (lead - 1ull));
+            if (!have && (need & lead) && next + rank < wend) {
+                i = next + rank;
+                have = true;
+                start_target();  // the single (inlined) initialisation site
+            }
+            next += __popcll(need);
+        }
+        if (__ballot(have) == 0) break;  // wave-uniform exit: range drained, every target written
+        if (!have || done) continue;
         Fr<T> root, L_;
         if (base) base_frame(root, b[0], b[1], b[2]);
         else set_identity(root);
@@ -201,7 +247,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_W
                 done = true;
             } else {
                 it = att * L + 1;
-                ik_start_attempt<T, MAXA>(S, a, q, ldq, off, gi, att, qs);
+                ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
                 b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
             }
             continue;
@@ -320,28 +366,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_W
             for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
         ++it;
     }
-    bool writer = final_lane;
-    if constexpr (G > 1) {
-        int gm = res_att;
-#pragma unroll
-        for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
-        writer = (gm != INT_MAX) ? (res_att == gm) : final_lane;
-    } else {
-        writer = valid;
-    }
-    if (!writer) return;
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        if (c >= 0) st_soa(q, c, ldq, off, qs[s]);
-    }
-    if (base)
-        for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
-    if (iters) iters[i] = it;
-    if (err) {
-        st_soa(err, 0, lde, off, ep);
-        st_soa(err, 1, lde, off, er);
-    }
 }
 
 // --------------------------------------------------------------------------
@@ -427,17 +451,35 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
                   0};
     const int G = ik_group(n, natt, a.lanes);
-    const int64_t chunk = kChunk / 8;  // lane index gt = i * G stays below 2^32
+    static const int64_t resident_waves = [] {  // 2 waves per SIMD: the IK kernels hold ~190 VGPRs
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return (int64_t)(cus > 0 ? cus : 256) * 8;
+    }();
+    const int64_t chunk = kChunk / 8;  // lane byte offsets i * sizeof(T) stay below 2^32
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = s0;
         const int64_t c = std::min(chunk, n - s0);
-        const dim3 grid(grid_of(c * G, 256)), block(256);
+        const int64_t ng = 64 / G;
+        // queue depth: one target per group (no refill) while the batch fills the chip in at most
+        // two rounds of waves, else as many waves as stay resident, each working through its share
+        static const int qmode = [] {
+            const char* e = getenv("KINHIP_IK_QUEUE");
+            return e ? atoi(e) : -1;
+        }();
+        const int64_t plain = (c + ng - 1) / ng;
+        const bool queue = qmode >= 0 ? qmode != 0 : plain > 2 * resident_waves;
+        const int64_t waves = queue ? std::min(resident_waves, plain) : plain;
+        const int64_t per_wave = (c + waves - 1) / waves;  // targets each wave works through
+        const int64_t nw = (c + per_wave - 1) / per_wave;
+        const dim3 grid((unsigned)((nw * 64 + 255) / 256)), block(256);
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
 #define KIN_IK_G(MA, R, GG) \
-        hipLaunchKernelGGL((k_ik_dls<T, MA, R, GG>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde)
+        hipLaunchKernelGGL((k_ik_dls<T, MA, R, GG>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde, per_wave)
 #define KIN_IK6(MA) \
         switch (G) { case 2: KIN_IK_G(MA, 6, 2); break; case 4: KIN_IK_G(MA, 6, 4); break; \
                      case 8: KIN_IK_G(MA, 6, 8); break; default: KIN_IK_G(MA, 6, 1); }

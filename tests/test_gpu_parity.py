@@ -326,6 +326,28 @@ def test_ik_dls_lanes_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0].cpu().numpy(), rq, atol=1e-7)
 
 
+def test_ik_dls_work_queue_identical(dev, fetch_tree):
+    """Large batches run as per-wave work queues (a lane group that finishes takes the wave's next
+    target): bit-identical to one target per group (lanes=1 here never queues), and the first
+    targets match the oracle."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 1 << 17
+    tgt = _targets(om, ids, gl.id, N, 41)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
+    T = torch.tensor(tgt, device=dev).contiguous()
+    kw = dict(max_iters=32, restarts=3, seed=9)
+    a = plan.ik_dls(T, torch.zeros((8, N), dtype=torch.float64, device=dev), lanes=4, **kw)
+    b = plan.ik_dls(T, torch.zeros((8, N), dtype=torch.float64, device=dev), lanes=1, **kw)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    k = 1500
+    rq, rit, _ = om.ik_dls_batch(np.zeros((8, k)), ids, gl.id, tgt[:, :k], **kw)
+    np.testing.assert_array_equal(a[1][:k].cpu().numpy(), rit)
+    np.testing.assert_allclose(a[0][:, :k].cpu().numpy(), rq, atol=1e-7)
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ik_dls_acceptance(dev, fetch_tree, dtype):
     """Reachable random targets: converged solutions meet the reference test's criteria

@@ -16,7 +16,7 @@ gl = m.find_link("gripper_link")
 out = []
 for dt in (torch.float32, torch.float64):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
-    n = 65536
+    n = int(os.environ.get("IK_N", 65536))
     Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=4242,
                                 dtype=dt, device=dev)
     tgt = plan.run(Qt)[0][0].contiguous()

@@ -18,6 +18,8 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--pad", type=int, default=256, help="row padding of the SoA buffers (as bench.py)")
 a = ap.parse_args()
+if a.what.startswith("ik") and a.n == 1 << 20:
+    a.n = 65536  # config 4 size
 dev = torch.device("cuda", 0)
 m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
 arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
@@ -55,6 +57,6 @@ else:
     tgt = T[0].contiguous()
     for _ in range(a.steps):
         Q0 = torch.zeros_like(Q)
-        plan.ik_dls(tgt, Q0, max_iters=64)
+        plan.ik_dls(tgt, Q0, max_iters=64, restarts=3, lam=1e-2, max_step=0.5)
 torch.cuda.synchronize()
 print("done", a.what, a.steps)

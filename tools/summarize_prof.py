@@ -22,6 +22,8 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "fkjac32": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20), "FK + 6x8 J, fp32, N = 2^20: 8 q in, 60 out"),
     "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
     "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
+    "ik32": ("k_ik_dls<float, 8, 6, 4>", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
+             "config 4: DLS IK, 65,536 targets, 64 iterations, 3 restarts, G = 4 lanes per target, fp32"),
     "coll32": ("k_coll<float, 8, false>", (8 + 1) * 4 * (1 << 20),
                "config 5 validity: FK + 14 spheres vs 7-box fridge SDF, min distance out, fp32, N = 2^20"),
     "collg32": ("k_coll<float, 8, true>", (8 + 14 + 14 * 8) * 4 * (1 << 20),
