@@ -350,6 +350,7 @@ def main():
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9}
         del p2, Q2, P2
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
+        out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream)
     if rank == 0 and not args.no_cpu:
