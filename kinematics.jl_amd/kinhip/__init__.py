@@ -7,15 +7,17 @@ fails loudly.
 """
 from ._lib import KinError, LIB_PATH, lib  # noqa: F401
 from .mechanism import (  # noqa: F401
-    BoxMetaData, Joint, Link, Mechanism, Plan, SphereMetaData, add_new_link, child_joints, child_link,
+    BoxMetaData, Joint, Link, Mechanism, Plan, SphereMetaData, Transform, add_new_link, child_joints, child_link,
     child_links, find_joint, find_link, get_jacobian, get_jacobian_, get_jacobian_batch, get_joint_angles,
-    get_transform, get_transform_batch, inverse_kinematics_, is_relevant, isleaf, isroot, parent_joint,
-    parent_link, parse_urdf, point_inverse_kinematics_nakamura, rpy, set_joint_angles,
+    get_joint_angles_, get_transform, get_transform_batch, inverse_kinematics_, is_relevant, isleaf, isroot,
+    joint_angle, parent_joint, parent_link, parse_urdf, point_inverse_kinematics_nakamura, rotation, rpy,
+    set_joint_angle, set_joint_angles, translation,
 )
 from .synth import uniform_configs  # noqa: F401
 from .collision import (  # noqa: F401
     FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, BoxSDF, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
-    add_coll_links, add_fetch_arm_spheres, compute_coll_dists, compute_coll_dists_and_grads, fridge_sdf,
+    add_coll_links, add_fetch_arm_spheres, compute_coll_dists, compute_coll_dists_, compute_coll_dists_and_grads,
+    compute_coll_dists_and_grads_, compute_swept_sphere, fridge_sdf,
 )
 from .planning import (  # noqa: F401
     ConfigurationConstraint, EqConst, IneqConst, Objective, PoseConstraint, construct_problem,

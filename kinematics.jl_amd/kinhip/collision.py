@@ -131,6 +131,29 @@ class CollisionPlan:
         return D, G, Mn
 
 
+def compute_coll_dists_(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, out_vals: np.ndarray):
+    """``compute_coll_dists!`` (src/collision.jl:51-58): fills out_vals in place."""
+    out_vals[:] = compute_coll_dists(sscc, joints, sdf)
+    return out_vals
+
+
+def compute_coll_dists_and_grads_(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, out_vals: np.ndarray,
+                                  out_grads: np.ndarray, truncation_dist=float("inf")):
+    """``compute_coll_dists_and_grads!`` (src/collision.jl:67-94): out_vals [n_sph], out_grads [n_dof, n_sph]."""
+    v, g = compute_coll_dists_and_grads(sscc, joints, sdf, truncation_dist=truncation_dist)
+    out_vals[:] = v
+    out_grads[:, :] = g
+    return out_vals, out_grads
+
+
+def compute_swept_sphere(link: Link):
+    """src/collision.jl:16-30 -> (centers [(x, y, z)], radii).  The reference fits spheres to the
+    link's collision mesh with skrobot + trimesh (offline-unavailable); this returns the
+    build-defined table entry (FETCH_LINK_SPHERES), or no spheres for a link it does not cover."""
+    entries = FETCH_LINK_SPHERES.get(link.name, [])
+    return [np.asarray(c, np.float64) for c, _ in entries], [float(r) for _, r in entries]
+
+
 def compute_coll_dists(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF) -> np.ndarray:
     """src/collision.jl:60-65 at the mechanism's current angles (GPU, batch of one)."""
     d, _ = compute_coll_dists_and_grads(sscc, joints, sdf, with_grad=False)

@@ -397,6 +397,22 @@ def get_joint_angles(m: Mechanism, joints):
     return m.get_joint_angles(joints)
 
 
+def get_joint_angles_(m: Mechanism, joints, out: np.ndarray) -> np.ndarray:
+    """``get_joint_angles!`` (src/mechanism.jl:203-221): fills `out` in place."""
+    out[:] = m.get_joint_angles(joints)
+    return out
+
+
+def joint_angle(m: Mechanism, joint: Joint) -> float:
+    """src/mechanism.jl:197."""
+    return m.joint_angle(joint)
+
+
+def set_joint_angle(m: Mechanism, joint: Joint, angle: float):
+    """src/mechanism.jl:199-201."""
+    m.set_joint_angle(joint, angle)
+
+
 def add_new_link(m: Mechanism, new_link: Link, parent: Link, pose_or_position):
     return m.add_new_link(new_link, parent, pose_or_position)
 
@@ -475,6 +491,27 @@ def get_jacobian_batch(m: Mechanism, link, joints, Q: torch.Tensor, with_rot=Tru
                   dtype=Q.dtype)
     poses, jac = plan.run(Q)
     return poses[0], jac
+
+
+def translation(T) -> np.ndarray:
+    """src/transform.jl:42: the translation of a 4x4 transform."""
+    return np.asarray(T, np.float64)[:3, 3].copy()
+
+
+def rotation(T) -> np.ndarray:
+    """src/transform.jl:43: the 3x3 rotation of a 4x4 transform."""
+    return np.asarray(T, np.float64)[:3, :3].copy()
+
+
+def Transform(rot=None, trans=None) -> np.ndarray:
+    """src/transform.jl:16-31: a 4x4 homogeneous transform from a 3x3 rotation and/or a translation
+    (identity parts where omitted; ``zero(Transform)`` is the identity, :50-52)."""
+    T = np.eye(4)
+    if rot is not None:
+        T[:3, :3] = np.asarray(rot, np.float64)
+    if trans is not None:
+        T[:3, 3] = np.asarray(trans, np.float64)
+    return T
 
 
 def rpy(T) -> np.ndarray:

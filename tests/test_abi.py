@@ -169,3 +169,28 @@ def test_synthetic_configs_are_shard_invariant():
     assert float(full[0].min()) >= 0 and float(full[0].max()) <= 0.4
     assert float(full[2].min()) >= -np.pi and float(full[2].max()) <= np.pi
     assert abs(float(full[1].mean())) < 0.1
+
+
+def test_reference_host_helpers():
+    """Host-side mirrors of the reference exports (src/transform.jl, src/mechanism.jl)."""
+    import numpy as np
+    import kinhip
+    import oracle as O
+    from conftest import golden
+    R = O.rpy_to_matrix([0.3, -0.4, 1.1])
+    T = kinhip.Transform(R, [1.0, 2.0, 3.0])
+    np.testing.assert_allclose(kinhip.rotation(T), R)
+    np.testing.assert_allclose(kinhip.translation(T), [1, 2, 3])
+    np.testing.assert_allclose(kinhip.rpy(T), O.rpy(T), atol=1e-15)
+    np.testing.assert_allclose(kinhip.rpy(T), [0.3, -0.4, 1.1], atol=1e-12)
+    np.testing.assert_array_equal(kinhip.Transform(), np.eye(4))
+    m = kinhip.parse_urdf(golden("fetch.urdf"))
+    j = m.find_joint("elbow_flex_joint")
+    kinhip.set_joint_angle(m, j, -0.7)
+    assert kinhip.joint_angle(m, j) == -0.7
+    out = np.zeros(2)
+    kinhip.get_joint_angles_(m, [m.find_joint("shoulder_pan_joint"), j], out)
+    np.testing.assert_array_equal(out, [0.0, -0.7])
+    c, r = kinhip.compute_swept_sphere(m.find_link("upperarm_roll_link"))
+    assert len(c) == len(r) == 2 and all(x > 0 for x in r)
+    assert kinhip.compute_swept_sphere(m.find_link("base_link")) == ([], [])
