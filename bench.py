@@ -58,6 +58,29 @@ def _time_plan(plan, Q, poses, jac, steps, warmup, ctx, stream):
     return wall, dev_s
 
 
+def _time_tiled(plan, Qt, n, poses, jac, steps, warmup, ctx, stream):
+    """_time_plan for kin_plan_run_tiled."""
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            plan.run_tiled(Qt, n, poses, jac, stream=stream)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        plan.run_tiled(Qt, n, poses, jac, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_s = e0.elapsed_time(e1) / 1e3
+    return D.max_over_ranks(ctx, [wall, dev_s])
+
+
 def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
     """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
     <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
@@ -243,13 +266,14 @@ def _copy_bw(dev, nbytes=1 << 31):
     return gbs
 
 
-def _pmc_traffic():
+def _pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), if present."""
     p = os.path.join(ROOT, "profiles", "pmc_fk_jac_f32.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
     return None
 
 
@@ -262,6 +286,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--extras", type=int, default=1, help="also time fp64 FK+J, config 2, IK and collision legs")
     ap.add_argument("--row-pad", type=int, default=256, help="elements of padding per SoA row (ld = n + pad)")
+    ap.add_argument("--layout", choices=["tiled", "soa"], default="tiled",
+                    help="headline layout: tiled SoA (kin_plan_run_tiled) or plain SoA rows (kin_plan_run)")
+    ap.add_argument("--tile", type=int, default=4096, help="configurations per tile of the tiled layout")
     ap.add_argument("--sweep", action="store_true", help="batch-size sweep, unpadded rows, strong scaling")
     args = ap.parse_args()
 
@@ -288,15 +315,40 @@ def main():
         J = torch.empty((8, 6, ld), dtype=dtype, device=dev)[:, :, :n] if jac else None
         return plan, Qb[:, :n], poses, J
 
+    def leg_tiled(dtype, jac, links, tile, n=N, start=None):
+        """Tiled SoA (kin_plan_run_tiled): (ntiles, rows, tile) arrays, one contiguous run per
+        output row and tile."""
+        plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
+                      with_rot=True, dtype=dtype)
+        Q = kinhip.uniform_configs(lo, hi, n, start=rank * n if start is None else start, dtype=dtype, device=dev)
+        Qt = kinhip.tiled(Q, tile)
+        nt = Qt.shape[0]
+        poses = torch.empty((nt, len(links), 12, tile), dtype=dtype, device=dev)
+        J = torch.empty((nt, 8, 6, tile), dtype=dtype, device=dev) if jac else None
+        return plan, Qt, poses, J
+
+    def timed_leg(dtype, jac, links, layout, n=N, start=None, steps=args.steps, warmup=args.warmup):
+        """(wall s, device s) of `steps` launches of one FK(+J) workload in `layout`:
+        "tiled" / "tileT" (kin_plan_run_tiled) or "soa" / "soa_padP" (kin_plan_run)."""
+        if layout.startswith("tile"):
+            tile = args.tile if layout == "tiled" else int(layout[4:])
+            plan, Qx, Px, Jx = leg_tiled(dtype, jac, links, tile, n=n, start=start)
+            r = _time_tiled(plan, Qx, n, Px, Jx, steps, warmup, ctx, stream)
+        else:
+            pad = args.row_pad if layout == "soa" else int(layout[7:])
+            plan, Qx, Px, Jx = leg(dtype, jac, links, n=n, pad=pad, start=start)
+            r = _time_plan(plan, Qx, Px, Jx, steps, warmup, ctx, stream)
+        del plan, Qx, Px, Jx
+        return r
+
     # ---- headline: FK + J, fp32 -------------------------------------------------
-    plan, Q, poses, J = leg(torch.float32, True, [gl])
-    wall, dev_s = _time_plan(plan, Q, poses, J, args.steps, args.warmup, ctx, stream)
+    wall, dev_s = timed_leg(torch.float32, True, [gl], args.layout)
     evals = N * ws * args.steps
     value = evals / wall
     bytes_per_eval = (8 + 12 + 48) * 4  # q in + pose + J out (algorithmic)
     t_launch = dev_s / args.steps
     achieved = bytes_per_eval * N / t_launch / 1e9
-    traffic = _pmc_traffic()
+    traffic = _pmc_traffic("fkjac32t" if args.layout == "tiled" else "fkjac32")
     out = {
         "metric": "FK+Jacobian evals/sec, Fetch URDF, batch=1M, at 1/2/4/8 MI355X",
         "value": value, "unit": "evals/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
@@ -311,44 +363,47 @@ def main():
                      "kernel": "k_fk<float,8>", "algorithmic_bytes_per_eval": bytes_per_eval,
                      "avg_launch_us": t_launch * 1e6},
     }
-    out["config"]["row_pad_elems"] = args.row_pad
+    if args.layout == "tiled":
+        out["config"]["layout"] = (f"tiled SoA, tile {args.tile} (kin_plan_run_tiled: Julia Array{{Float32,3}}"
+                                   f"({args.tile}, rows, N/{args.tile}))")
+    else:
+        out["config"]["layout"] = f"plain SoA (kin_plan_run), rows padded to ld = N + {args.row_pad}"
     if args.extras:
         out["roofline"]["measured_copy_GBs"] = _copy_bw(dev)
+    if args.extras:
+        # the same workload in the other layouts: plain SoA (padded and unpadded rows), other tiles
+        lay = {}
+        for name in ("soa_pad%d" % args.row_pad, "soa_pad0", "tile2048", "tile4096", "tile8192"):
+            wt, dt_ = timed_leg(torch.float32, True, [gl], name)
+            lay[name] = {"value": N * ws * args.steps / wt, "unit": "evals/s", "avg_launch_us": dt_ / args.steps * 1e6,
+                         "achieved_GBs": bytes_per_eval * N / (dt_ / args.steps) / 1e9}
+        out["fk_jac_f32_layouts"] = lay
     if args.sweep:
         # batch sweep: launch-overhead vs bandwidth regime, fp32 FK + J
         sweep = {}
         for lg in range(16, 27, 2):
-            for pad in (0, args.row_pad):
+            for name in ("soa_pad0", "soa_pad%d" % args.row_pad, "tile%d" % args.tile):
                 n_s = 1 << lg
-                ps, Qs, Ps, Js = leg(torch.float32, True, [gl], n=n_s, pad=pad)
                 k_s = max(5, min(50, (1 << 26) // n_s))
-                ws_, ds_ = _time_plan(ps, Qs, Ps, Js, k_s, 3, ctx, stream)
-                sweep[f"2^{lg}+{pad}"] = {"evals_per_s": n_s * ws * k_s / ws_, "avg_launch_us": ds_ / k_s * 1e6,
-                                          "achieved_GBs": bytes_per_eval * n_s / (ds_ / k_s) / 1e9}
-                del ps, Qs, Ps, Js
+                ws_, ds_ = timed_leg(torch.float32, True, [gl], name, n=n_s, steps=k_s, warmup=3)
+                sweep[f"2^{lg} {name}"] = {"evals_per_s": n_s * ws * k_s / ws_, "avg_launch_us": ds_ / k_s * 1e6,
+                                           "achieved_GBs": bytes_per_eval * n_s / (ds_ / k_s) / 1e9}
         out["batch_sweep_fk_jac_f32"] = sweep
     if ws > 1:  # strong scaling: one global 2^20 batch split across the ranks
         st0, cnt = D.split_range(N, rank, ws)
-        ps, Qs, Ps, Js = leg(torch.float32, True, [gl], n=cnt, start=st0)
-        w_s, d_s = _time_plan(ps, Qs, Ps, Js, args.steps, args.warmup, ctx, stream)
+        w_s, d_s = timed_leg(torch.float32, True, [gl], args.layout, n=cnt, start=st0)
         out["strong_scaling_fk_jac_f32"] = {"global_batch": N, "value": N * args.steps / w_s, "unit": "evals/s",
                                             "ms_per_step": w_s / args.steps * 1e3}
-        del ps, Qs, Ps, Js
     if args.extras:
         # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
-        p64, Q64, P64, J64 = leg(torch.float64, True, [gl])
-        w64, d64 = _time_plan(p64, Q64, P64, J64, max(5, args.steps // 2), 3, ctx, stream)
-        out["fp64_fk_jac"] = {"value": N * ws * max(5, args.steps // 2) / w64, "unit": "evals/s",
-                              "avg_launch_us": d64 / max(5, args.steps // 2) * 1e6,
-                              "achieved_GBs": 544 * N / (d64 / max(5, args.steps // 2)) / 1e9}
-        del p64, Q64, P64, J64
-        links = [m.find_link(n) for n in EXAMPLE_LINKS]
-        p2, Q2, P2, _ = leg(torch.float64, False, links)
-        w2, d2 = _time_plan(p2, Q2, P2, None, max(5, args.steps // 2), 3, ctx, stream)
         k2 = max(5, args.steps // 2)
+        w64, d64 = timed_leg(torch.float64, True, [gl], args.layout, steps=k2, warmup=3)
+        out["fp64_fk_jac"] = {"value": N * ws * k2 / w64, "unit": "evals/s", "avg_launch_us": d64 / k2 * 1e6,
+                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": args.layout}
+        links = [m.find_link(n) for n in EXAMPLE_LINKS]
+        w2, d2 = timed_leg(torch.float64, False, links, args.layout, steps=k2, warmup=3)
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
-                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9}
-        del p2, Q2, P2
+                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": args.layout}
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))

@@ -164,6 +164,18 @@ KINHIP_API int kin_plan_shape(const kin_plan* p, int32_t* n_qcols, int32_t* jac_
 KINHIP_API int kin_plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n,
                             void* poses, int64_t ldp, void* jac, int64_t ldj, void* stream);
 
+/* Tiled structure-of-arrays variant of kin_plan_run (the MI355X-preferred
+ * layout for large batches): configurations are grouped in
+ * tiles of `tile` (a multiple of 256, <= 2^26); element (config i, row r) of an
+ * array X lives at X[(i / tile) * ts + r * ld + (i % tile)], i.e. a Julia
+ * Array{T,3}(ld, rows, ntiles) with ld >= tile and ts >= rows * ld (the last
+ * tile may be partial).  tile >= n is exactly kin_plan_run.  Each workgroup
+ * then writes one contiguous tile-row run per output row instead of 60 streams
+ * 4 MB apart (profiles/r01_tile_probe.txt: +10% HBM rate for FK + J). */
+KINHIP_API int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q, int64_t ldq, int64_t tsq, int64_t n,
+                                  void* poses, int64_t ldp, int64_t tsp, void* jac, int64_t ldj, int64_t tsj,
+                                  void* stream);
+
 /* One-shot conveniences with an internal per-model plan cache (the first call
  * for a request stages it synchronously; later calls are async).
  * kin_get_transform_batch: poses of n_out links.  kin_get_jacobian_batch: the

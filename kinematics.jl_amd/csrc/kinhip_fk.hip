@@ -12,12 +12,18 @@ template <typename T, int MAXA>
 __global__ __launch_bounds__(256) void k_fk(const KProg<T> P, const KStep<T>* __restrict__ S,
                                             const T* __restrict__ q, int64_t ldq, int64_t n,
                                             T* __restrict__ poses, int64_t ldp, T* __restrict__ jac,
-                                            int64_t ldj) {
+                                            int64_t ldj, const Tiling tl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* slots = reinterpret_cast<T*>(smem);
     const int B = blockDim.x, tid = threadIdx.x;
-    const uint32_t i = config_block() * (uint32_t)B + tid;
-    if (i >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
+    const uint32_t b = config_block();
+    if ((uint64_t)b * (uint32_t)B + tid >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
+    // tiled SoA: this workgroup's tile (wave-uniform) moves the array bases; lanes keep a 32-bit offset
+    const uint32_t t = b / tl.tile_blocks;
+    if (q) q += (int64_t)t * tl.tsq;
+    if (poses) poses += (int64_t)t * tl.tsp;
+    if (jac) jac += (int64_t)t * tl.tsj;
+    const uint32_t i = (b - t * tl.tile_blocks) * (uint32_t)B + tid;
     const uint32_t off = i * (uint32_t)sizeof(T);
     Sink<T> sk;
     sk.off = off;
@@ -168,15 +174,21 @@ __global__ __launch_bounds__(256) void k_pose_residual(const T* __restrict__ pos
 
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
-                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, hipStream_t st) {
-    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
-        const int64_t c = std::min(kChunk, n - s0);
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipStream_t st) {
+    // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
+    const bool tiled = ta.tile < n;
+    const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
+    Tiling tl{tiled ? (uint32_t)(ta.tile / g.block) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj};
+    for (int64_t s0 = 0; s0 < n; s0 += chunk) {
+        const int64_t c = std::min(chunk, n - s0);
         const dim3 grid(grid_of(c, g.block)), block(g.block);
-        const T* qc = q ? q + s0 : q;
-        T* pc = poses ? poses + s0 : poses;
-        T* jc = jac ? jac + s0 : jac;
+        const int64_t tq = tiled ? (s0 / ta.tile) * ta.tsq : s0, tp = tiled ? (s0 / ta.tile) * ta.tsp : s0,
+                      tj = tiled ? (s0 / ta.tile) * ta.tsj : s0;
+        const T* qc = q ? q + tq : q;
+        T* pc = poses ? poses + tp : poses;
+        T* jc = jac ? jac + tj : jac;
 #define KIN_FK_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_fk<T, MA>), grid, block, g.lds, st, P, steps, qc, ldq, c, pc, ldp, jc, ldj)
+        hipLaunchKernelGGL((k_fk<T, MA>), grid, block, g.lds, st, P, steps, qc, ldq, c, pc, ldp, jc, ldj, tl)
         KIN_MAXA_DISPATCH(g.maxA, KIN_FK_LAUNCH)
 #undef KIN_FK_LAUNCH
         const hipError_t e = hipGetLastError();
@@ -200,7 +212,7 @@ hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, in
 
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_fk<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, \
-                                     int64_t, T*, int64_t, T*, int64_t, hipStream_t);                        \
+                                     int64_t, T*, int64_t, T*, int64_t, const TileArgs&, hipStream_t);       \
     template hipError_t launch_pose_residual<T>(const T*, int64_t, const T*, int64_t, int64_t, int, T*, int64_t, \
                                                 hipStream_t);
 KIN_INSTANTIATE(float)

@@ -945,24 +945,46 @@ int kin_plan_shape(const kin_plan* p, int32_t* nq, int32_t* rows, int32_t* cols)
     return KIN_OK;
 }
 
-int kin_plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* poses, int64_t ldp, void* jac,
-                 int64_t ldj, void* stream) {
-    if (!p) return set_error(KIN_E_INVALID, "kin_plan_run: null plan");
-    if (n < 0) return set_error(KIN_E_INVALID, "kin_plan_run: n < 0");
+namespace {
+int plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* poses, int64_t ldp, void* jac,
+             int64_t ldj, const TileArgs& ta, void* stream, const char* fn) {
+    auto bad = [&](const char* what) { return set_error(KIN_E_INVALID, std::string(fn) + ": " + what); };
+    if (!p) return bad("null plan");
+    if (n < 0) return bad("n < 0");
     if (n == 0) return KIN_OK;
-    if (p->nqcols > 0 && (!dev_ptr_ok(q) || ldq < n)) return set_error(KIN_E_INVALID, "kin_plan_run: bad q / ldq");
-    if (p->n_out > 0 && !poses) return set_error(KIN_E_INVALID, "kin_plan_run: null poses");
-    if (poses && ldp < n) return set_error(KIN_E_INVALID, "kin_plan_run: ldp < n");
-    if (p->has_jac && (!jac || ldj < n)) return set_error(KIN_E_INVALID, "kin_plan_run: bad jac / ldj");
+    const int64_t span = std::min(ta.tile, n);  // configurations along one row of one tile
+    if (p->nqcols > 0 && (!dev_ptr_ok(q) || ldq < span)) return bad("bad q / ldq");
+    if (p->n_out > 0 && !poses) return bad("null poses");
+    if (poses && ldp < span) return bad("ldp < tile");
+    if (p->has_jac && (!jac || ldj < span)) return bad("bad jac / ldj");
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_fk<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)q, ldq, n, (float*)poses,
-                             ldp, (float*)jac, ldj, (hipStream_t)stream);
+                             ldp, (float*)jac, ldj, ta, (hipStream_t)stream);
     else
         e = launch_fk<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)q, ldq, n,
-                              (double*)poses, ldp, (double*)jac, ldj, (hipStream_t)stream);
+                              (double*)poses, ldp, (double*)jac, ldj, ta, (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_fk launch: ") + hipGetErrorString(e));
     return KIN_OK;
+}
+}  // namespace
+
+int kin_plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* poses, int64_t ldp, void* jac,
+                 int64_t ldj, void* stream) {
+    return plan_run(p, q, ldq, n, poses, ldp, jac, ldj, plain_soa(n), stream, "kin_plan_run");
+}
+
+int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q, int64_t ldq, int64_t tsq, int64_t n,
+                       void* poses, int64_t ldp, int64_t tsp, void* jac, int64_t ldj, int64_t tsj, void* stream) {
+    auto bad = [&](const char* what) { return set_error(KIN_E_INVALID, std::string("kin_plan_run_tiled: ") + what); };
+    if (!p) return bad("null plan");
+    if (tile < 256 || tile % 256 != 0 || tile > (int64_t(1) << 26)) return bad("tile must be a multiple of 256 <= 2^26");
+    if (n > tile) {  // several tiles: their strides must not overlap a tile's rows
+        if (p->nqcols > 0 && tsq < (int64_t)p->nqcols * ldq) return bad("tsq < n_qcols * ldq");
+        if (p->n_out > 0 && tsp < (int64_t)p->n_out * 12 * ldp) return bad("tsp < n_out * 12 * ldp");
+        if (p->has_jac && tsj < (int64_t)p->ncols * p->rows * ldj) return bad("tsj < cols * rows * ldj");
+    }
+    return plan_run(p, q, ldq, n, poses, ldp, jac, ldj, TileArgs{tile, tsq, tsp, tsj}, stream, "kin_plan_run_tiled");
 }
 
 int kin_get_transform_batch(kin_model* m, int32_t dtype, int32_t n_q, const int32_t* qids, const void* q,

@@ -15,9 +15,17 @@ struct LaunchGeom {
     int maxA;       // phase-A steps as compiled (4 / 8 / 12 / 16 / 32); the program is padded to it
 };
 
+// Tiled SoA (kin_plan_run_tiled): element (i, r) of an array at (i / tile) * ts + r * ld + i % tile.
+// tile >= n is the plain SoA of kin_plan_run (one tile, ts unused).
+struct TileArgs {
+    int64_t tile;
+    int64_t tsq, tsp, tsj;  // tile strides (elements) of q, poses, jac
+};
+inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0}; }
+
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
-                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, hipStream_t st);
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipStream_t st);
 
 struct IkArgs {
     int32_t max_iters;

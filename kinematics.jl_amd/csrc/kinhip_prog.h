@@ -81,6 +81,12 @@ struct KAabb {
     T pad[2];
 };
 
+// kernel-side tiling: workgroup b works on tile b / tile_blocks (0xffffffff: plain SoA)
+struct Tiling {
+    uint32_t tile_blocks;
+    int64_t tsq, tsp, tsj;
+};
+
 template <typename T>
 struct KProg {
     int32_t nA;        // phase-A steps (root -> spine link, padded to the kernel's MAXA)

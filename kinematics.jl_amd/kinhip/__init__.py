@@ -11,7 +11,7 @@ from .mechanism import (  # noqa: F401
     child_links, find_joint, find_link, get_jacobian, get_jacobian_, get_jacobian_batch, get_joint_angles,
     get_joint_angles_, get_transform, get_transform_batch, inverse_kinematics_, is_relevant, isleaf, isroot,
     joint_angle, parent_joint, parent_link, parse_urdf, point_inverse_kinematics_nakamura, rotation, rpy,
-    set_joint_angle, set_joint_angles, translation,
+    set_joint_angle, set_joint_angles, tiled, translation, untiled,
 )
 from .synth import uniform_configs  # noqa: F401
 from .collision import (  # noqa: F401

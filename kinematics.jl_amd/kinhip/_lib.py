@@ -31,7 +31,7 @@ EXPORTS = [
     "kin_urdf_parse_file", "kin_urdf_parse_string", "kin_urdf_destroy", "kin_urdf_tree",
     "kin_urdf_link_name", "kin_urdf_joint_name", "kin_urdf_find_link", "kin_urdf_find_joint",
     "kin_urdf_link_box",
-    "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run",
+    "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run", "kin_plan_run_tiled",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
@@ -108,6 +108,7 @@ def lib():
         "kin_plan_destroy": ([P], C.c_int),
         "kin_plan_shape": ([P, P, P, P], C.c_int),
         "kin_plan_run": ([P, P, I64, I64, P, I64, P, I64, P], C.c_int),
+        "kin_plan_run_tiled": ([P, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P], C.c_int),
         "kin_get_transform_batch": ([P, I32, I32, P, P, I64, I64, I32, P, P, I64, P], C.c_int),
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),
         "kin_ik_dls_batch": ([P, P, P, I64, P, I64, I64, P, P, I64, P], C.c_int),

@@ -277,6 +277,41 @@ class Plan:
                                      jac.data_ptr() if jac is not None else None, ldj, st))
         return poses, jac
 
+    def run_tiled(self, Qt: torch.Tensor, n: int, poses: Optional[torch.Tensor] = None,
+                  jac: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None):
+        """kin_plan_run_tiled: the tiled-SoA layout (include/kinhip.h).  Qt is (ntiles, n_qcols, tile)
+        with unit configuration stride (``tiled(Q, tile)``); outputs are (ntiles, n_out, 12, tile) and
+        (ntiles, cols, rows, tile).  `n` <= ntiles * tile configurations are evaluated.  Async."""
+        if not Qt.is_cuda or Qt.dtype != self.dtype or Qt.dim() != 3 or Qt.shape[1] != self.n_qcols:
+            raise ValueError(f"Qt must be a CUDA {self.dtype} tensor of shape (ntiles, {self.n_qcols}, tile)")
+        nt, _, tile = Qt.shape
+        if Qt.stride(2) != 1 or not 0 <= n <= nt * tile:
+            raise ValueError("Qt must be configuration-contiguous and hold n configurations")
+        dev = Qt.device
+        if poses is None and self.n_out:
+            poses = torch.empty((nt, self.n_out, 12, tile), dtype=self.dtype, device=dev)
+        if jac is None and self._jl:
+            alloc = torch.zeros if not self.zero_fill else torch.empty
+            jac = alloc((nt, self.jac_cols, self.jac_rows, tile), dtype=self.dtype, device=dev)
+
+        def geom(t, shape):
+            if t is None:
+                return None, tile, 0
+            if tuple(t.shape) != shape or t.dtype != self.dtype or not t.is_cuda or t.stride(3) != 1:
+                raise ValueError(f"tiled output must be a CUDA {self.dtype} tensor of shape {shape}")
+            a, b = shape[1], shape[2]
+            ld = t.stride(2)
+            if a > 1 and t.stride(1) != b * ld:
+                raise ValueError("tiled output rows must be evenly spaced")
+            return t.data_ptr(), ld, t.stride(0)
+
+        pp, ldp, tsp = geom(poses, (nt, self.n_out, 12, tile))
+        jp, ldj, tsj = geom(jac, (nt, self.jac_cols, self.jac_rows, tile))
+        st = (stream or torch.cuda.current_stream(dev)).cuda_stream
+        K.check(K.lib().kin_plan_run_tiled(self._h, tile, Qt.data_ptr() if self.n_qcols else None, Qt.stride(1),
+                                           Qt.stride(0), n, pp, ldp, tsp, jp, ldj, tsj, st))
+        return poses, jac
+
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
                max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, stream=None):
         """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
@@ -415,6 +450,21 @@ def set_joint_angle(m: Mechanism, joint: Joint, angle: float):
 
 def add_new_link(m: Mechanism, new_link: Link, parent: Link, pose_or_position):
     return m.add_new_link(new_link, parent, pose_or_position)
+
+
+def tiled(X: torch.Tensor, tile: int) -> torch.Tensor:
+    """[..., N] SoA -> [ntiles, ..., tile] tiled SoA (N padded up to a whole number of tiles)."""
+    n = X.shape[-1]
+    nt = -(-n // tile)
+    if nt * tile != n:
+        X = torch.nn.functional.pad(X, (0, nt * tile - n))
+    return X.reshape(*X.shape[:-1], nt, tile).movedim(-2, 0).contiguous()
+
+
+def untiled(Xt: torch.Tensor, n: int) -> torch.Tensor:
+    """Inverse of tiled(): [ntiles, ..., tile] -> [..., n]."""
+    X = Xt.movedim(0, -2)
+    return X.reshape(*X.shape[:-2], -1)[..., :n]
 
 
 def _ld_of(t: torch.Tensor, shape, dtype) -> int:

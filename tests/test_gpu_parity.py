@@ -203,6 +203,45 @@ def test_edge_sizes_and_strides(dev, fetch_tree):
     plan.run(torch.empty((8, 0), dtype=torch.float64, device=dev))
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_tiled_layout(dev, fetch_tree, dtype, with_base):
+    """kin_plan_run_tiled: (ntiles, rows, tile) layout == plain SoA bit for bit, and vs the oracle;
+    partial last tile, one tile, row padding inside a tile, phase-B links."""
+    m, arm = _fetch(with_base)
+    gl = m.find_link("gripper_link")
+    links = [gl] + [m.find_link(n) for n in EXAMPLE_LINKS]
+    plan = m.plan(arm, out_links=links, jac_link=gl, dtype=dtype)
+    om = O.OracleMech(fetch_tree, with_base=with_base)
+    for N, tile in ((3000, 256), (5000, 1024), (700, 1024), (4096, 4096)):
+        Q = _rand_q(N, plan.n_qcols, N + tile, dtype, dev)
+        P0, J0 = plan.run(Q)
+        Pt, Jt = plan.run_tiled(kinhip.tiled(Q, tile), N)
+        assert torch.equal(kinhip.untiled(Pt, N), P0) and torch.equal(kinhip.untiled(Jt, N), J0)
+        ps, js = om.fk_jac_batch(Q.double().cpu().numpy(), [j.id for j in arm], gl.id, [j.id for j in arm])
+        np.testing.assert_allclose(kinhip.untiled(Jt, N).double().cpu().numpy(), js, atol=TOL[dtype])
+        np.testing.assert_allclose(kinhip.untiled(Pt, N)[0].double().cpu().numpy(), ps, atol=TOL[dtype])
+    # rows padded inside each tile (ld > tile) and tiles padded apart (ts > rows * ld)
+    N, tile = 2000, 512
+    Q = _rand_q(N, plan.n_qcols, 1, dtype, dev)
+    nt = -(-N // tile)
+    Qt = torch.zeros((nt, plan.n_qcols, tile + 64), dtype=dtype, device=dev)
+    Qt[:, :, :tile] = kinhip.tiled(Q, tile)
+    Pb = torch.full((nt + 1, len(links), 12, tile + 32), 7.0, dtype=dtype, device=dev)
+    Jb = torch.full((nt, plan.jac_cols + 1, 6, tile + 96), 7.0, dtype=dtype, device=dev)
+    Pv = Pb[:nt, :, :, :tile]
+    Jv = Jb[:, :plan.jac_cols, :, :tile]
+    plan.run_tiled(Qt[:, :, :tile], N, poses=Pv, jac=Jv)
+    P0, J0 = plan.run(Q)
+    assert torch.equal(kinhip.untiled(Pv.contiguous(), N), P0)
+    assert torch.equal(kinhip.untiled(Jv.contiguous(), N), J0)
+    assert bool((Pb[nt] == 7.0).all()) and bool((Jb[:, plan.jac_cols] == 7.0).all())
+    assert bool((Pb[..., tile:] == 7.0).all()) and bool((Jb[..., tile:] == 7.0).all())
+    # bad tilings are refused, never launched
+    with pytest.raises(kinhip.KinError):
+        plan.run_tiled(torch.zeros((2, plan.n_qcols, 100), dtype=dtype, device=dev), 200)
+
+
 def test_large_batch_properties(dev, fetch_tree):
     """BASELINE size (2^20, fp32): size-independent properties + a strided oracle sample."""
     m, arm = _fetch()

@@ -13,10 +13,11 @@ sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac64", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
+ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--pad", type=int, default=256, help="row padding of the SoA buffers (as bench.py)")
+ap.add_argument("--tile", type=int, default=4096, help="tile of the tiled-SoA workloads (*t, as bench.py)")
 a = ap.parse_args()
 if a.what.startswith("ik") and a.n == 1 << 20:
     a.n = 65536  # config 4 size
@@ -24,10 +25,18 @@ dev = torch.device("cuda", 0)
 m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
 arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
 gl = m.find_link("gripper_link")
-dt = torch.float64 if a.what.endswith("64") else torch.float32
+dt = torch.float64 if "64" in a.what else torch.float32
 Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], a.n, dtype=dt, device=dev)
 ld = a.n + a.pad
-if a.what.startswith("fkjac"):
+if a.what.startswith("fkjac") and a.what.endswith("t"):
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    Qt = kinhip.tiled(Q, a.tile)
+    nt = Qt.shape[0]
+    P = torch.empty((nt, 1, 12, a.tile), dtype=dt, device=dev)
+    J = torch.empty((nt, 8, 6, a.tile), dtype=dt, device=dev)
+    for _ in range(a.steps):
+        plan.run_tiled(Qt, a.n, P, J)
+elif a.what.startswith("fkjac"):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     Qb = torch.empty((8, ld), dtype=dt, device=dev)
     Qb[:, :a.n] = Q
