@@ -288,7 +288,10 @@ def main():
     ap.add_argument("--row-pad", type=int, default=256, help="elements of padding per SoA row (ld = n + pad)")
     ap.add_argument("--layout", choices=["tiled", "soa"], default="tiled",
                     help="headline layout: tiled SoA (kin_plan_run_tiled) or plain SoA rows (kin_plan_run)")
-    ap.add_argument("--tile", type=int, default=4096, help="configurations per tile of the tiled layout")
+    ap.add_argument("--tile", type=int, default=8192, help="configurations per tile of the tiled layout")
+    ap.add_argument("--layout64", choices=["tiled", "soa"], default="tiled", help="layout of the fp64 legs")
+    ap.add_argument("--spec", type=int, default=1,
+                    help="1: plan-specialised kernels (kin_plan_specialize), 0: the generic kernels")
     ap.add_argument("--sweep", action="store_true", help="batch-size sweep, unpadded rows, strong scaling")
     args = ap.parse_args()
 
@@ -301,12 +304,16 @@ def main():
     lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
     stream = torch.cuda.Stream(dev)
 
-    def leg(dtype, jac, links, n=N, pad=args.row_pad, start=None):
+    def mkplan(dtype, jac, links, spec):
+        plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
+                      with_rot=True, dtype=dtype)
+        return plan.specialize() if spec else plan
+
+    def leg(dtype, jac, links, n=N, pad=args.row_pad, start=None, spec=args.spec):
         """Device-resident SoA buffers; every row padded to ld = n + pad elements (the C-ABI's
         ldq / ldp / ldj): rows exactly 2^k elements apart line all 68 streams of a wave up on the
         same HBM channels (tools/ld_probe.py, profiles/r01_row_pad_probe.txt)."""
-        plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
-                      with_rot=True, dtype=dtype)
+        plan = mkplan(dtype, jac, links, spec)
         ld = n + pad
         Qb = torch.empty((8, ld), dtype=dtype, device=dev)
         Qb[:, :n] = kinhip.uniform_configs(lo, hi, n, start=rank * n if start is None else start, dtype=dtype,
@@ -315,11 +322,10 @@ def main():
         J = torch.empty((8, 6, ld), dtype=dtype, device=dev)[:, :, :n] if jac else None
         return plan, Qb[:, :n], poses, J
 
-    def leg_tiled(dtype, jac, links, tile, n=N, start=None):
+    def leg_tiled(dtype, jac, links, tile, n=N, start=None, spec=args.spec):
         """Tiled SoA (kin_plan_run_tiled): (ntiles, rows, tile) arrays, one contiguous run per
         output row and tile."""
-        plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, jac_joints=arm if jac else None,
-                      with_rot=True, dtype=dtype)
+        plan = mkplan(dtype, jac, links, spec)
         Q = kinhip.uniform_configs(lo, hi, n, start=rank * n if start is None else start, dtype=dtype, device=dev)
         Qt = kinhip.tiled(Q, tile)
         nt = Qt.shape[0]
@@ -329,14 +335,18 @@ def main():
 
     def timed_leg(dtype, jac, links, layout, n=N, start=None, steps=args.steps, warmup=args.warmup):
         """(wall s, device s) of `steps` launches of one FK(+J) workload in `layout`:
-        "tiled" / "tileT" (kin_plan_run_tiled) or "soa" / "soa_padP" (kin_plan_run)."""
+        "tiled" / "tileT" (kin_plan_run_tiled) or "soa" / "soa_padP" (kin_plan_run); a "generic_"
+        prefix runs the generic (not plan-specialised) kernel."""
+        spec = args.spec
+        if layout.startswith("generic_"):
+            spec, layout = 0, layout[8:]
         if layout.startswith("tile"):
             tile = args.tile if layout == "tiled" else int(layout[4:])
-            plan, Qx, Px, Jx = leg_tiled(dtype, jac, links, tile, n=n, start=start)
+            plan, Qx, Px, Jx = leg_tiled(dtype, jac, links, tile, n=n, start=start, spec=spec)
             r = _time_tiled(plan, Qx, n, Px, Jx, steps, warmup, ctx, stream)
         else:
             pad = args.row_pad if layout == "soa" else int(layout[7:])
-            plan, Qx, Px, Jx = leg(dtype, jac, links, n=n, pad=pad, start=start)
+            plan, Qx, Px, Jx = leg(dtype, jac, links, n=n, pad=pad, start=start, spec=spec)
             r = _time_plan(plan, Qx, Px, Jx, steps, warmup, ctx, stream)
         del plan, Qx, Px, Jx
         return r
@@ -348,7 +358,7 @@ def main():
     bytes_per_eval = (8 + 12 + 48) * 4  # q in + pose + J out (algorithmic)
     t_launch = dev_s / args.steps
     achieved = bytes_per_eval * N / t_launch / 1e9
-    traffic = _pmc_traffic("fkjac32t" if args.layout == "tiled" else "fkjac32")
+    traffic = _pmc_traffic(("fkjac32t" if args.layout == "tiled" else "fkjac32") + ("s" if args.spec else ""))
     out = {
         "metric": "FK+Jacobian evals/sec, Fetch URDF, batch=1M, at 1/2/4/8 MI355X",
         "value": value, "unit": "evals/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup,
@@ -360,9 +370,12 @@ def main():
                    "parallelism": f"dp{ws} (independent shards)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_fk<float,8>", "algorithmic_bytes_per_eval": bytes_per_eval,
+                     "kernel": "kinhip_jit_fk (k_fk body specialised to the Fetch plan)" if args.spec else
+                     "k_fk<float, 8>", "algorithmic_bytes_per_eval": bytes_per_eval,
                      "avg_launch_us": t_launch * 1e6},
     }
+    out["config"]["kernels"] = ("plan-specialised (kin_plan_specialize: program constants folded by hiprtc)"
+                                if args.spec else "generic (program read from device memory)")
     if args.layout == "tiled":
         out["config"]["layout"] = (f"tiled SoA, tile {args.tile} (kin_plan_run_tiled: Julia Array{{Float32,3}}"
                                    f"({args.tile}, rows, N/{args.tile}))")
@@ -373,11 +386,17 @@ def main():
     if args.extras:
         # the same workload in the other layouts: plain SoA (padded and unpadded rows), other tiles
         lay = {}
-        for name in ("soa_pad%d" % args.row_pad, "soa_pad0", "tile2048", "tile4096", "tile8192"):
+        for name in ("soa_pad%d" % args.row_pad, "soa_pad0", "tile2048", "tile4096", "tile8192",
+                     "generic_soa_pad%d" % args.row_pad, "generic_tile4096", "generic_tile8192"):
             wt, dt_ = timed_leg(torch.float32, True, [gl], name)
             lay[name] = {"value": N * ws * args.steps / wt, "unit": "evals/s", "avg_launch_us": dt_ / args.steps * 1e6,
                          "achieved_GBs": bytes_per_eval * N / (dt_ / args.steps) / 1e9}
         out["fk_jac_f32_layouts"] = lay
+        for name in ("generic_soa", "generic_tiled", "soa"):  # fp64: the layout matters more
+            w_, d_ = timed_leg(torch.float64, True, [gl], name, steps=max(5, args.steps // 2), warmup=3)
+            lay[name + "_f64"] = {"value": N * ws * max(5, args.steps // 2) / w_, "unit": "evals/s",
+                                  "avg_launch_us": d_ / max(5, args.steps // 2) * 1e6,
+                                  "achieved_GBs": 544 * N / (d_ / max(5, args.steps // 2)) / 1e9}
     if args.sweep:
         # batch sweep: launch-overhead vs bandwidth regime, fp32 FK + J
         sweep = {}
@@ -397,13 +416,15 @@ def main():
     if args.extras:
         # fp64 FK+J (reference precision) and config 2 (FK of 6 links, fp64)
         k2 = max(5, args.steps // 2)
-        w64, d64 = timed_leg(torch.float64, True, [gl], args.layout, steps=k2, warmup=3)
+        # (fp64 rows are 8 B per lane: the tiled layout keeps each output row of a workgroup in one
+        # run and is 10-13% faster here than plain rows, fk_jac_f32_layouts *_f64)
+        w64, d64 = timed_leg(torch.float64, True, [gl], args.layout64, steps=k2, warmup=3)
         out["fp64_fk_jac"] = {"value": N * ws * k2 / w64, "unit": "evals/s", "avg_launch_us": d64 / k2 * 1e6,
-                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": args.layout}
+                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": args.layout64}
         links = [m.find_link(n) for n in EXAMPLE_LINKS]
-        w2, d2 = timed_leg(torch.float64, False, links, args.layout, steps=k2, warmup=3)
+        w2, d2 = timed_leg(torch.float64, False, links, args.layout64, steps=k2, warmup=3)
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
-                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": args.layout}
+                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": args.layout64}
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))

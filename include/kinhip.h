@@ -176,6 +176,21 @@ KINHIP_API int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q
                                   void* poses, int64_t ldp, int64_t tsp, void* jac, int64_t ldj, int64_t tsj,
                                   void* stream);
 
+/* Plan specialisation: compiles this plan's staged program at run time
+ * (hiprtc, gfx950) into kernels in which every fixed transform coefficient,
+ * joint kind, output index and Jacobian column is a compile-time constant --
+ * zero terms of the 3x4 products vanish and each joint's motion is chosen
+ * statically.  Afterwards the plan's launches of the selected kernels use the
+ * specialised code.  `kernels` is a mask of KIN_SPEC_* (0 = every kind that
+ * applies to the plan).  Synchronous (seconds on first use; code objects are
+ * cached per process by program text); call outside stream capture.  Results
+ * equal the generic kernels' for finite inputs, up to the sign of zeros.
+ * KIN_E_DEVICE (message from hiprtc) leaves the plan on its generic kernels. */
+enum { KIN_SPEC_FK = 1u };
+KINHIP_API int kin_plan_specialize(kin_plan* p, uint32_t kernels);
+/* The KIN_SPEC_* mask the plan currently runs specialised. */
+KINHIP_API int kin_plan_specialized(const kin_plan* p, uint32_t* kernels);
+
 /* One-shot conveniences with an internal per-model plan cache (the first call
  * for a request stages it synchronously; later calls are async).
  * kin_get_transform_batch: poses of n_out links.  kin_get_jacobian_batch: the

@@ -23,14 +23,25 @@
 // No MFMA: 3x4 rigid products are not a dense contraction; the kernels are
 // HBM-bound at the sizes of BASELINE.json (roofline).
 #pragma once
+#ifndef __HIPCC_RTC__  // run-time compiled sources (kinhip_jit.cpp) get only the device code
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 
 #include <algorithm>
 
 #include "kinhip_internal.h"
+#else
+#ifndef INT_MAX
+#define INT_MAX 2147483647
+#endif
+#ifndef INFINITY
+#define INFINITY __builtin_inff()
+#endif
+#endif
+#include "kinhip_prog.h"
 
 
 
@@ -142,6 +153,25 @@ __device__ __forceinline__ void set_identity(Fr<T>& f) {
     f.t[0] = f.t[1] = f.t[2] = T(0);
 }
 
+// Products with a coefficient of the staged program.  In the generic kernels
+// the coefficient is a run-time (uniform) value and these are plain fma/mul.
+// In plan-specialised kernels (kinhip_jit.cpp) it is a compile-time constant:
+// a term with an exactly-zero coefficient is dropped and `acc + 0` is not
+// formed, which the IEEE rules would otherwise keep (x * 0 is NaN for x = inf,
+// x + 0 flips -0).  For finite inputs the result equals the generic one (up to
+// the sign of a zero).
+template <typename T>
+__device__ __forceinline__ T fmz(T a, T F, T acc) {
+    if (__builtin_constant_p(F) && F == T(0)) return acc;
+    if (__builtin_constant_p(acc) && acc == T(0)) return a * F;
+    return fma(a, F, acc);
+}
+template <typename T>
+__device__ __forceinline__ T mulz(T a, T F) {
+    if (__builtin_constant_p(F) && F == T(0)) return T(0);
+    return a * F;
+}
+
 // f <- f * F   (F: row-major 3x4 in uniform memory)
 template <typename T>
 __device__ __forceinline__ void mul_rigid(Fr<T>& f, const T* __restrict__ F) {
@@ -152,10 +182,10 @@ __device__ __forceinline__ void mul_rigid(Fr<T>& f, const T* __restrict__ F) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
-        g.r[3 * i + 0] = fma(a, F0, fma(b, F4, c * F8));
-        g.r[3 * i + 1] = fma(a, F1, fma(b, F5, c * F9));
-        g.r[3 * i + 2] = fma(a, F2, fma(b, F6, c * F10));
-        g.t[i] = fma(a, F3, fma(b, F7, fma(c, F11, f.t[i])));
+        g.r[3 * i + 0] = fmz(a, F0, fmz(b, F4, mulz(c, F8)));
+        g.r[3 * i + 1] = fmz(a, F1, fmz(b, F5, mulz(c, F9)));
+        g.r[3 * i + 2] = fmz(a, F2, fmz(b, F6, mulz(c, F10)));
+        g.t[i] = fmz(a, F3, fmz(b, F7, fmz(c, F11, f.t[i])));
     }
     f = g;
 }
@@ -165,10 +195,10 @@ __device__ __forceinline__ void mul_rigid_regs(Fr<T>& out, const Fr<T>& f, const
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         const T a = f.r[3 * i], b = f.r[3 * i + 1], c = f.r[3 * i + 2];
-        out.r[3 * i + 0] = fma(a, F[0], fma(b, F[4], c * F[8]));
-        out.r[3 * i + 1] = fma(a, F[1], fma(b, F[5], c * F[9]));
-        out.r[3 * i + 2] = fma(a, F[2], fma(b, F[6], c * F[10]));
-        out.t[i] = fma(a, F[3], fma(b, F[7], fma(c, F[11], f.t[i])));
+        out.r[3 * i + 0] = fmz(a, F[0], fmz(b, F[4], mulz(c, F[8])));
+        out.r[3 * i + 1] = fmz(a, F[1], fmz(b, F[5], mulz(c, F[9])));
+        out.r[3 * i + 2] = fmz(a, F[2], fmz(b, F[6], mulz(c, F[10])));
+        out.t[i] = fmz(a, F[3], fmz(b, F[7], fmz(c, F[11], f.t[i])));
     }
 }
 
@@ -176,6 +206,31 @@ __device__ __forceinline__ void mul_rigid_regs(Fr<T>& out, const Fr<T>& f, const
 // joint kind: revolute -> (c, s, 0), prismatic -> (1, 0, scale*q), none -> (1, 0, 0)
 template <typename T>
 __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T scale, T qv) {
+    if (__builtin_constant_p(kind) && __builtin_constant_p(flags)) {  // specialised plan: kind known
+        if (kind == MOT_REV) {
+            T th = qv;
+            if (flags & SF_SCALE) {
+                T sh, ch;
+                sincos_t(T(0.5) * qv, &sh, &ch);
+                th = T(2) * atan2_t(scale * sh, ch);
+            }
+            T s, c;
+            sincos_t(th, &s, &c);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const T a = f.r[3 * i], b = f.r[3 * i + 1];
+                f.r[3 * i] = fma(a, c, b * s);
+                f.r[3 * i + 1] = fma(b, c, -(a * s));
+            }
+        } else if (kind == MOT_PRISM) {
+            const T d = scale * qv;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) f.t[i] = fma(f.r[3 * i + 2], d, f.t[i]);
+        }
+        return;
+    }
+    // generic: branch-free in the kind (a uniform branch per step splits the
+    // unrolled chain into blocks and costs more than it saves, profiles/r01_fk_branch_ab.txt)
     const bool rev = kind == MOT_REV;
     T th = rev ? qv : T(0);
     if (flags & SF_SCALE) {  // UnitQuaternion normalisation of a non-unit axis

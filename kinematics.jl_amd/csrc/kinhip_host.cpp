@@ -188,7 +188,13 @@ struct kin_plan {
     void* d_sph = nullptr;
     // spheres on several chains: one staged program per chain (kin_coll_plan_create)
     std::vector<std::unique_ptr<kin_plan>> parts;
+    // host copy of the staged program (plan specialisation, kinhip_jit.cpp)
+    std::vector<unsigned char> h_steps;
+    int32_t n_steps = 0;
+    JitKernels* jit = nullptr;
+    uint32_t jit_mask = 0;
     ~kin_plan() {
+        jit_destroy(jit);
         if (d_steps) (void)hipFree(d_steps);
         if (d_sph) (void)hipFree(d_sph);
     }
@@ -708,6 +714,8 @@ struct Stager {
             host.assign(bytes, 0);
             fill(P.pd, reinterpret_cast<KStep<double>*>(host.data()));
         }
+        P.h_steps = host;
+        P.n_steps = (int32_t)steps.size();
         hipError_t e = hipMalloc(&P.d_steps, bytes);
         if (e != hipSuccess) {
             P.d_steps = nullptr;
@@ -960,10 +968,10 @@ int plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* pos
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_fk<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)q, ldq, n, (float*)poses,
-                             ldp, (float*)jac, ldj, ta, (hipStream_t)stream);
+                             ldp, (float*)jac, ldj, ta, jit_fk(p->jit), (hipStream_t)stream);
     else
         e = launch_fk<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)q, ldq, n,
-                              (double*)poses, ldp, (double*)jac, ldj, ta, (hipStream_t)stream);
+                              (double*)poses, ldp, (double*)jac, ldj, ta, jit_fk(p->jit), (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_fk launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }
@@ -985,6 +993,32 @@ int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q, int64_t l
         if (p->has_jac && tsj < (int64_t)p->ncols * p->rows * ldj) return bad("tsj < cols * rows * ldj");
     }
     return plan_run(p, q, ldq, n, poses, ldp, jac, ldj, TileArgs{tile, tsq, tsp, tsj}, stream, "kin_plan_run_tiled");
+}
+
+int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
+    if (!p) return set_error(KIN_E_INVALID, "kin_plan_specialize: null plan");
+    uint32_t applies = p->is_coll ? 0u : KIN_SPEC_FK;
+    if (kernels == 0) kernels = applies;
+    if (kernels & ~applies) return set_error(KIN_E_UNSUPPORTED, "kin_plan_specialize: kernel kind does not apply");
+    if (kernels == 0 || (p->jit_mask & kernels) == kernels) return KIN_OK;
+    kernels |= p->jit_mask;
+    JitKernels* k = nullptr;
+    const int rc = p->dtype == KIN_F32
+                       ? jit_build<float>(p->pf, (const KStep<float>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
+                                          kernels, &k)
+                       : jit_build<double>(p->pd, (const KStep<double>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
+                                           kernels, &k);
+    if (rc != KIN_OK) return rc;
+    jit_destroy(p->jit);
+    p->jit = k;
+    p->jit_mask = kernels;
+    return KIN_OK;
+}
+
+int kin_plan_specialized(const kin_plan* p, uint32_t* kernels) {
+    if (!p || !kernels) return set_error(KIN_E_INVALID, "kin_plan_specialized: null argument");
+    *kernels = p->jit_mask;
+    return KIN_OK;
 }
 
 int kin_get_transform_batch(kin_model* m, int32_t dtype, int32_t n_q, const int32_t* qids, const void* q,

@@ -1,8 +1,20 @@
 // kinhip_host.h -- internal host helpers shared by the C-ABI translation units.
 #pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
 #include <string>
+
+#include "kinhip_prog.h"
 
 namespace kinhip {
 // Records a thread-local message for kin_last_error() and returns code.
 int set_error(int code, const std::string& msg);
+
+// plan specialisation (kinhip_jit.cpp): kernels compiled for one staged program
+struct JitKernels;
+template <typename T>
+int jit_build(const KProg<T>& P, const KStep<T>* steps, int nsteps, int maxA, uint32_t kernels, JitKernels** out);
+void jit_destroy(JitKernels* k);
+hipFunction_t jit_fk(const JitKernels* k);
 }  // namespace kinhip

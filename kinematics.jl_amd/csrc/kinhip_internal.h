@@ -23,9 +23,11 @@ struct TileArgs {
 };
 inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0}; }
 
+// jit: the plan-specialised kernel (kinhip_jit.cpp) or null for the generic one
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
-                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipStream_t st);
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipFunction_t jit,
+                     hipStream_t st);
 
 struct IkArgs {
     int32_t max_iters;

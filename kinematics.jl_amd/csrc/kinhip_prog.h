@@ -18,7 +18,14 @@
 // batch column, at m.angles) are pre-multiplied on the host in fp64 exactly
 // like joint_transform does it (quaternion path, `angle == 0.0` shortcut).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else
+using __hip_internal::int32_t;  // hiprtc's fixed-width types
+using __hip_internal::int64_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 namespace kinhip {
 

@@ -22,6 +22,7 @@ KIN_E_UNSUPPORTED, KIN_E_NOMEM, KIN_E_PARSE, KIN_E_IO = -5, -6, -7, -8
 KIN_F32, KIN_F64 = 0, 1
 KIN_JOINT_FIXED, KIN_JOINT_REVOLUTE, KIN_JOINT_PRISMATIC = 0, 1, 2
 KIN_WITH_ROT, KIN_RPY_JAC, KIN_ZERO_FILL = 1, 2, 4
+KIN_SPEC_FK = 1
 
 # every entry point include/kinhip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -32,6 +33,7 @@ EXPORTS = [
     "kin_urdf_link_name", "kin_urdf_joint_name", "kin_urdf_find_link", "kin_urdf_find_joint",
     "kin_urdf_link_box",
     "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run", "kin_plan_run_tiled",
+    "kin_plan_specialize", "kin_plan_specialized",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
@@ -108,6 +110,8 @@ def lib():
         "kin_plan_destroy": ([P], C.c_int),
         "kin_plan_shape": ([P, P, P, P], C.c_int),
         "kin_plan_run": ([P, P, I64, I64, P, I64, P, I64, P], C.c_int),
+        "kin_plan_specialize": ([P, U32], C.c_int),
+        "kin_plan_specialized": ([P, P], C.c_int),
         "kin_plan_run_tiled": ([P, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P], C.c_int),
         "kin_get_transform_batch": ([P, I32, I32, P, P, I64, I64, I32, P, P, I64, P], C.c_int),
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),

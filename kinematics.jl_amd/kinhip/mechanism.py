@@ -251,6 +251,18 @@ class Plan:
             K._lib.kin_plan_destroy(self._h)
             self._h = None
 
+    def specialize(self, kernels: int = 0) -> "Plan":
+        """kin_plan_specialize: compile this plan's program into constant-folded gfx950 kernels
+        (hiprtc; synchronous, cached per process).  Returns self."""
+        K.check(K.lib().kin_plan_specialize(self._h, int(kernels)))
+        return self
+
+    @property
+    def specialized(self) -> int:
+        v = C.c_uint32()
+        K.check(K.lib().kin_plan_specialized(self._h, C.byref(v)))
+        return v.value
+
     def _check_q(self, Q: torch.Tensor) -> int:
         if not Q.is_cuda or Q.dtype != self.dtype or Q.dim() != 2 or Q.shape[0] != self.n_qcols:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_qcols}, N)")

@@ -242,6 +242,55 @@ def test_tiled_layout(dev, fetch_tree, dtype, with_base):
         plan.run_tiled(torch.zeros((2, plan.n_qcols, 100), dtype=dtype, device=dev), 200)
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("rpy_jac", [False, True])
+def test_specialized_fk_equals_generic(dev, fetch_tree, dtype, with_base, rpy_jac):
+    """kin_plan_specialize: the constant-folded kernel gives the generic kernel's results (values
+    equal; only the sign of a zero may differ) for FK + J, phase-B links, plain and tiled layouts."""
+    m, arm = _fetch(with_base)
+    gl = m.find_link("gripper_link")
+    links = [gl] + [m.find_link(n) for n in EXAMPLE_LINKS] + [m.find_link("head_camera_rgb_optical_frame")]
+    N = 3001
+    Q = _rand_q(N, 8 + (3 if with_base else 0), 17, dtype, dev)
+    gen = m.plan(arm, out_links=links, jac_link=gl, rpy_jac=rpy_jac, dtype=dtype)
+    spe = m.plan(arm, out_links=links, jac_link=gl, rpy_jac=rpy_jac, dtype=dtype)
+    assert spe.specialized == 0
+    spe.specialize()
+    assert spe.specialized == kinhip.KIN_SPEC_FK
+    P0, J0 = gen.run(Q)
+    P1, J1 = spe.run(Q)
+    assert torch.equal(P0, P1) and torch.equal(J0, J1)
+    Pt, Jt = spe.run_tiled(kinhip.tiled(Q, 1024), N)
+    assert torch.equal(kinhip.untiled(Pt, N), P0) and torch.equal(kinhip.untiled(Jt, N), J0)
+    om = O.OracleMech(fetch_tree, with_base=with_base)
+    ps, js = om.fk_jac_batch(Q.double().cpu().numpy(), [j.id for j in arm], gl.id, [j.id for j in arm], True,
+                             rpy_jac)
+    np.testing.assert_allclose(P1[0].double().cpu().numpy(), ps, atol=TOL[dtype])
+
+
+def test_specialized_column_semantics(dev, fetch_tree):
+    """Specialised plans honour m.angles of non-batched joints, repeated / irrelevant columns and
+    get_jacobian! (untouched) vs get_jacobian (zeros) like the generic ones."""
+    m, arm = _fetch()
+    head = m.find_joint("head_pan_joint")
+    jj = [arm[3], head, arm[0], arm[3], arm[6]]
+    gl = m.find_link("gripper_link")
+    qj = arm[:5]
+    for j, a in zip(arm[5:], [0.4, -0.7, 1.1]):
+        m.set_joint_angle(j, a)
+    Q = _rand_q(700, 5, 3, torch.float64, dev)
+    for zero in (True, False):
+        gen = m.plan(qj, out_links=[gl], jac_link=gl, jac_joints=jj, zero_fill=zero, dtype=torch.float64)
+        spe = m.plan(qj, out_links=[gl], jac_link=gl, jac_joints=jj, zero_fill=zero, dtype=torch.float64)
+        spe.specialize(kinhip.KIN_SPEC_FK)
+        a = torch.full((len(jj), 6, 700), 9.0, dtype=torch.float64, device=dev)
+        b = a.clone()
+        gen.run(Q, jac=a)
+        spe.run(Q, jac=b)
+        assert torch.equal(a, b)
+
+
 def test_large_batch_properties(dev, fetch_tree):
     """BASELINE size (2^20, fp32): size-independent properties + a strided oracle sample."""
     m, arm = _fetch()

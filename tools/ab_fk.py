@@ -32,8 +32,14 @@ def timed(fn, k=100):
     return e0.elapsed_time(e1) / k * 1e3
 
 
+import time
+SPEC = int(os.environ.get("AB_SPEC", "0"))
 for dt, esz in ((torch.float32, 4), (torch.float64, 8)):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if SPEC:
+        t0 = time.perf_counter()
+        plan.specialize()
+        res.append(f"spec {time.perf_counter() - t0:.2f}s")
     Q = kinhip.uniform_configs(lo, hi, N, dtype=dt, device=dev)
     ld = N + 256
     Qb = torch.empty((8, ld), dtype=dt, device=dev)
@@ -49,4 +55,4 @@ for dt, esz in ((torch.float32, 4), (torch.float64, 8)):
     us = timed(lambda: plan.run_tiled(Qt, N, Pt, Jt))
     res.append(f"tile4096 {us:6.2f}us {68 * esz * N / us / 1e3:5.0f}GB/s")
     del Qt, Pt, Jt
-print(os.path.basename(os.environ.get("KINHIP_LIB", "default")).ljust(20), " | ".join(res), flush=True)
+print((os.path.basename(os.environ.get("KINHIP_LIB", "default")) + (" spec" if SPEC else "")).ljust(20), " | ".join(res), flush=True)

@@ -13,12 +13,15 @@ sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
+ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fkjac32s", "fkjac32ts", "fkjac64ts", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--pad", type=int, default=256, help="row padding of the SoA buffers (as bench.py)")
-ap.add_argument("--tile", type=int, default=4096, help="tile of the tiled-SoA workloads (*t, as bench.py)")
+ap.add_argument("--tile", type=int, default=8192, help="tile of the tiled-SoA workloads (*t, as bench.py)")
 a = ap.parse_args()
+SPEC = a.what.endswith("s") and a.what.startswith("fk")  # plan-specialised kernel (kin_plan_specialize)
+if SPEC:
+    a.what = a.what[:-1]
 if a.what.startswith("ik") and a.n == 1 << 20:
     a.n = 65536  # config 4 size
 dev = torch.device("cuda", 0)
@@ -30,6 +33,8 @@ Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in
 ld = a.n + a.pad
 if a.what.startswith("fkjac") and a.what.endswith("t"):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if SPEC:
+        plan.specialize()
     Qt = kinhip.tiled(Q, a.tile)
     nt = Qt.shape[0]
     P = torch.empty((nt, 1, 12, a.tile), dtype=dt, device=dev)
@@ -38,6 +43,8 @@ if a.what.startswith("fkjac") and a.what.endswith("t"):
         plan.run_tiled(Qt, a.n, P, J)
 elif a.what.startswith("fkjac"):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if SPEC:
+        plan.specialize()
     Qb = torch.empty((8, ld), dtype=dt, device=dev)
     Qb[:, :a.n] = Q
     Q = Qb[:, :a.n]

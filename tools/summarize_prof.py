@@ -21,8 +21,14 @@ OUT = os.path.join(ROOT, "profiles")
 WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "fkjac32": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20), "FK + 6x8 J, fp32, N = 2^20: 8 q in, 60 out"),
     "fkjac32t": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20),
-                 "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile 4096; the bench headline layout)"),
+                 "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile as run), generic kernel"),
     "fkjac64t": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile 4096)"),
+    "fkjac32s": ("kinhip_jit_fk", (8 + 12 + 48) * 4 * (1 << 20),
+                 "FK + 6x8 J, fp32, N = 2^20, plain SoA rows padded by 256, plan-specialised kernel"),
+    "fkjac32ts": ("kinhip_jit_fk", (8 + 12 + 48) * 4 * (1 << 20),
+                  "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile 8192), plan-specialised kernel (bench headline)"),
+    "fkjac64ts": ("kinhip_jit_fk", (8 + 12 + 48) * 8 * (1 << 20),
+                  "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile as run), plan-specialised kernel"),
     "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
     "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
     "ik32": ("k_ik_dls<float, 8, 6, 4>", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
@@ -96,7 +102,7 @@ def main():
                        "20 launches each via tools/prof_kernel.py; hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950)"}
         with open(os.path.join(OUT, f"{a.round}_pmc_{tag}.json"), "w") as f:
             json.dump(d, f, indent=1)
-        if tag == "fkjac32t":  # the headline kernel's PMC pass, read by bench.py (roofline.traffic)
+        if tag == "fkjac32ts":  # the headline kernel's PMC pass, read by bench.py (roofline.traffic)
             with open(os.path.join(OUT, "pmc_fk_jac_f32.json"), "w") as f:
                 json.dump(d, f, indent=1)
         print(json.dumps({k: d[k] for k in ("workload", "hbm_bytes_per_launch", "traffic_over_algorithmic",
@@ -104,7 +110,7 @@ def main():
     b = os.path.join(PROF, "bench", "bench_kernel_stats.csv")
     if os.path.exists(b):
         shutil.copy(b, os.path.join(OUT, f"{a.round}_bench_kernel_stats.csv"))
-        print("bench:", stats(b, "k_fk<float, 8>"))
+        print("bench:", stats(b, "kinhip_jit_fk"))
 
 
 if __name__ == "__main__":
