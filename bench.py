@@ -81,13 +81,15 @@ def _time_tiled(plan, Qt, n, poses, jac, steps, warmup, ctx, stream):
     return D.max_over_ranks(ctx, [wall, dev_s])
 
 
-def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
+def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5, spec=1):
     """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
     <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
     Multi-GPU: the solutions (8 angles) and iteration counts are all-gathered to every rank over
     RCCL afterwards -- timed separately, not part of the solve rate."""
     dt = torch.float32
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if spec:
+        plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
     start, cnt = D.shard_range(n, ctx.rank)
     Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], cnt, start=start,
                                 seed=4242, dtype=dt, device=ctx.device)
@@ -109,7 +111,8 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
     succ = (it < 64).float().mean()
     out = {"value": n * ctx.world * reps / wall, "unit": "IK solves/s", "targets_per_gpu": n,
            "success_rate": float(succ), "ms_per_batch": wall / reps * 1e3, "dtype": "f32",
-           "params": "DLS lambda=1e-2, max_step=0.5, 64 iters incl. 3 seeded restarts, q0=0"}
+           "params": "DLS lambda=1e-2, max_step=0.5, 64 iters incl. 3 seeded restarts, q0=0",
+           "kernels": "specialised" if spec else "generic"}
     if ctx.world > 1:
         torch.cuda.synchronize()
         D.barrier(ctx)
@@ -123,7 +126,7 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5):
     return out
 
 
-def _coll_leg(ctx, stream, n, steps):
+def _coll_leg(ctx, stream, n, steps, spec=1):
     """Config 5: FK + SDF validity samples of the planner (src/planning.jl collision check):
     Fetch arm (8 joints) with 14 build-defined spheres vs the 7-box fridge scene (door at 2.0 rad,
     base at (1.2, 0, 0)), `n` configurations per GPU, fp32.  Two kernels: min-distance only
@@ -137,6 +140,8 @@ def _coll_leg(ctx, stream, n, steps):
     sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
     arm = [m.find_joint(n_) for n_ in ARM]
     plan = sscc.plan(arm, dtype=dt)
+    if spec:
+        plan.specialize()
     Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, start=ctx.rank * n,
                                seed=555, dtype=dt, device=ctx.device)
     out = {}
@@ -173,15 +178,17 @@ def _coll_leg(ctx, stream, n, steps):
                 out[name]["gather_ms"] = D.max_over_ranks(ctx, [(time.perf_counter() - g0) * 1e3])[0]
                 assert allv.shape[1] == n * ctx.world
     out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
-                       f"samples sharded across ranks")
+                       f"samples sharded across ranks, {'specialised' if spec else 'generic'} kernels")
     return out
 
 
-def _nakamura_leg(m, arm, gl, ctx, stream, n=1 << 18, reps=5):
+def _nakamura_leg(m, arm, gl, ctx, stream, n=1 << 18, reps=5, spec=1):
     """point_inverse_kinematics_nakamura (50 SR-inverse iterations, the reference's
     `.+ 1.0` quirk), fp64 as the reference, `n` reachable points per GPU from q0 = 0."""
     dt = torch.float64
     plan = m.plan(arm, out_links=[gl], jac_link=gl, jac_joints=arm, with_rot=False, dtype=dt)
+    if spec:
+        plan.specialize()
     start, cnt = D.shard_range(n, ctx.rank)
     Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], cnt, start=start,
                                 seed=99, dtype=dt, device=ctx.device)
@@ -202,7 +209,7 @@ def _nakamura_leg(m, arm, gl, ctx, stream, n=1 << 18, reps=5):
     err = (got - pts).norm(dim=0)
     return {"value": n * ctx.world * reps / wall, "unit": "point-IK solves/s (50 iterations each)",
             "points_per_gpu": n, "ms_per_batch": wall / reps * 1e3, "dtype": "f64",
-            "median_residual_m": float(err.median())}
+            "median_residual_m": float(err.median()), "kernels": "specialised" if spec else "generic"}
 
 
 def _cpu_model():
@@ -392,7 +399,7 @@ def main():
             lay[name] = {"value": N * ws * args.steps / wt, "unit": "evals/s", "avg_launch_us": dt_ / args.steps * 1e6,
                          "achieved_GBs": bytes_per_eval * N / (dt_ / args.steps) / 1e9}
         out["fk_jac_f32_layouts"] = lay
-        for name in ("generic_soa", "generic_tiled", "soa"):  # fp64: the layout matters more
+        for name in ("generic_soa", "generic_tile4096", "soa", "tile8192"):  # fp64: the layout matters more
             w_, d_ = timed_leg(torch.float64, True, [gl], name, steps=max(5, args.steps // 2), warmup=3)
             lay[name + "_f64"] = {"value": N * ws * max(5, args.steps // 2) / w_, "unit": "evals/s",
                                   "avg_launch_us": d_ / max(5, args.steps // 2) * 1e6,
@@ -418,17 +425,25 @@ def main():
         k2 = max(5, args.steps // 2)
         # (fp64 rows are 8 B per lane: the tiled layout keeps each output row of a workgroup in one
         # run and is 10-13% faster here than plain rows, fk_jac_f32_layouts *_f64)
-        w64, d64 = timed_leg(torch.float64, True, [gl], args.layout64, steps=k2, warmup=3)
+        lay64 = "tile%d" % (args.tile // 2) if args.layout64 == "tiled" else "soa"  # same bytes per tile row
+        w64, d64 = timed_leg(torch.float64, True, [gl], lay64, steps=k2, warmup=3)
         out["fp64_fk_jac"] = {"value": N * ws * k2 / w64, "unit": "evals/s", "avg_launch_us": d64 / k2 * 1e6,
-                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": args.layout64}
+                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": lay64}
         links = [m.find_link(n) for n in EXAMPLE_LINKS]
-        w2, d2 = timed_leg(torch.float64, False, links, args.layout64, steps=k2, warmup=3)
+        w2, d2 = timed_leg(torch.float64, False, links, lay64, steps=k2, warmup=3)
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
-                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": args.layout64}
-        out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream)
-        out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3)
-        out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2))
-        out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream)
+                                  "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": lay64}
+        out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec)
+        out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
+        out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec)
+        out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
+        if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)
+            out["generic_kernels"] = {
+                "config4_ik_dls": _ik_leg(m, arm, gl, ctx, stream, spec=0)["value"],
+                "ik_dls_1M_targets": _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=0)["value"],
+                "config5_fk_sdf": {k: v["value"] for k, v in _coll_leg(ctx, stream, N, max(5, args.steps // 2),
+                                                                        spec=0).items() if isinstance(v, dict)},
+                "a11_nakamura_f64": _nakamura_leg(m, arm, gl, ctx, stream, spec=0)["value"]}
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = _cpu_baseline(m)
     if rank == 0:

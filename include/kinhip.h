@@ -183,10 +183,17 @@ KINHIP_API int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q
  * statically.  Afterwards the plan's launches of the selected kernels use the
  * specialised code.  `kernels` is a mask of KIN_SPEC_* (0 = every kind that
  * applies to the plan).  Synchronous (seconds on first use; code objects are
- * cached per process by program text); call outside stream capture.  Results
- * equal the generic kernels' for finite inputs, up to the sign of zeros.
+ * cached per process by program text); call outside stream capture.  FK,
+ * Jacobian and collision results equal the generic kernels' for finite inputs
+ * (up to the sign of zeros); iterative IK may differ in the last bits where
+ * the two compilations contract a product-sum differently.
  * KIN_E_DEVICE (message from hiprtc) leaves the plan on its generic kernels. */
-enum { KIN_SPEC_FK = 1u };
+enum {
+    KIN_SPEC_FK = 1u,        /* kin_plan_run(_tiled), kin_get_*_batch, kin_pose_const_batch */
+    KIN_SPEC_IK = 2u,        /* kin_ik_dls_batch (with_rot 0/1, every lane count) */
+    KIN_SPEC_NAKAMURA = 4u,  /* kin_point_ik_nakamura_batch */
+    KIN_SPEC_COLL = 8u       /* kin_coll_batch, kin_ineq_const_batch (spheres folded; boxes stay data) */
+};
 KINHIP_API int kin_plan_specialize(kin_plan* p, uint32_t kernels);
 /* The KIN_SPEC_* mask the plan currently runs specialised. */
 KINHIP_API int kin_plan_specialized(const kin_plan* p, uint32_t* kernels);

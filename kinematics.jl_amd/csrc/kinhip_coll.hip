@@ -1,214 +1,20 @@
 // kinhip_coll.hip -- k_coll: swept spheres vs a union of box SDFs, fused with FK.
 // (gfx950 only; shared helpers in kinhip_device.h)
-#include "kinhip_device.h"
+#include "kinhip_coll_dev.h"
 
 namespace kinhip {
 namespace {
 
 // --------------------------------------------------------------------------
-// k_coll: compute_coll_dists_and_grads! (src/collision.jl:51-94) fused with FK:
-// sphere centres from the phase-A frames, UnionSDF (min over BoxSDFs,
-// src/sdf.jl:67-114) minus radius, gradient = grad_sdf^T J(3 x n) of the sphere
-// link from the recorded joint origins / axes.  The SDF gradient is analytic
-// (the reference takes a forward difference with eps 1e-7, src/sdf.jl:34-41;
-// equal to it up to O(eps) away from the box's kinks).
+// generic kernel (the staged program is read from device memory)
 // --------------------------------------------------------------------------
-// Monotone surrogate of the box SDF, d*|d|: outside (max q > 0) |max(q,0)|^2,
-// inside -(max q)^2.  The union takes the argmin of the surrogate (no square
-// root per box; sqrt(fl(x*x)) == |x| recovers an inside distance exactly).
-template <typename T>
-__device__ __forceinline__ T box_key(T qx, T qy, T qz) {
-    const T mx = fmax(qx, fmax(qy, qz));
-    const T ox = fmax(qx, T(0)), oy = fmax(qy, T(0)), oz = fmax(qz, T(0));
-    const T mn = fmin(mx, T(0));  // 0 outside, max(q) inside (where every o is 0)
-    return fma(ox, ox, fma(oy, oy, fma(oz, oz, -(mn * mn))));
-}
-
-// d from its surrogate d|d|: one square root (hardware v_sqrt_f32 for fp32, <= 1 ulp)
-__device__ __forceinline__ float signed_sqrt(float k) { return copysignf(__builtin_amdgcn_sqrtf(fabsf(k)), k); }
-__device__ __forceinline__ double signed_sqrt(double k) { return copysign(sqrt(fabs(k)), k); }
-
-#ifndef KINHIP_AABB_UNROLL
-#define KINHIP_AABB_UNROLL 2
-#endif
-template <typename T, bool GRAD>
-__device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
-                                       int nb, T px, T py, T pz, T (&gw)[3]) {
-    T best = T(INFINITY);
-    int bk = 0;
-    // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
-#pragma clang loop vectorize(disable) unroll_count(KINHIP_AABB_UNROLL)
-    for (int k = 0; k < na; ++k) {  // axis-aligned boxes: no rotation
-        const KAabb<T>& b = aabb[k];
-        const T key = box_key(fabs(px - b.c[0]) - b.half[0], fabs(py - b.c[1]) - b.half[1],
-                              fabs(pz - b.c[2]) - b.half[2]);
-        if (GRAD) {
-            if (key < best) {
-                best = key;
-                bk = k;
-            }
-        } else {
-            best = fmin(best, key);
-        }
-    }
-#pragma clang loop vectorize(disable)
-    for (int k = na; k < nb; ++k) {
-        const KBox<T>& b = boxes[k];
-        const T qx = fabs(fma(b.inv[0], px, fma(b.inv[1], py, fma(b.inv[2], pz, b.inv[3])))) - b.half[0];
-        const T qy = fabs(fma(b.inv[4], px, fma(b.inv[5], py, fma(b.inv[6], pz, b.inv[7])))) - b.half[1];
-        const T qz = fabs(fma(b.inv[8], px, fma(b.inv[9], py, fma(b.inv[10], pz, b.inv[11])))) - b.half[2];
-        const T key = box_key(qx, qy, qz);
-        if (GRAD) {
-            if (key < best) {
-                best = key;
-                bk = k;
-            }
-        } else {
-            best = fmin(best, key);
-        }
-    }
-    const T d = signed_sqrt(best);
-    if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
-        const KBox<T>& b = boxes[bk];
-        T l[3], q[3], gl[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            l[i] = fma(b.inv[4 * i], px, fma(b.inv[4 * i + 1], py, fma(b.inv[4 * i + 2], pz, b.inv[4 * i + 3])));
-            q[i] = fabs(l[i]) - b.half[i];
-        }
-        const T mx = fmax(q[0], fmax(q[1], q[2]));
-        if (mx > T(0)) {  // outside: d = |max(q, 0)|
-            const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
-            const T rn = T(1) / sqrt_t(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] = (l[i] < T(0) ? -o[i] : o[i]) * rn;
-        } else {  // inside: d = max(q)
-            const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] = (i == im) ? (l[i] < T(0) ? T(-1) : T(1)) : T(0);
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) gw[j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
-    }
-    return d;
-}
-
-template <typename T, int MAXA, bool GRAD>
-__device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
-                                             const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
-                                             const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb,
-                                             int na, int nb, T trunc, T offs,
-                                             const T (&rm)[MAXA][3], const T (&rz)[MAXA][3], T bx, T by,
-                                             uint32_t off, T* __restrict__ dists, int64_t ldd,
-                                             T* __restrict__ grads, int64_t ldg, T& dmin) {
-    const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
-    for (int k = k0; k < k1; ++k) {
-        const KSphere<T>& sp = sph[k];
-        const T px = fma(f.r[0], sp.c[0], fma(f.r[1], sp.c[1], fma(f.r[2], sp.c[2], f.t[0])));
-        const T py = fma(f.r[3], sp.c[0], fma(f.r[4], sp.c[1], fma(f.r[5], sp.c[2], f.t[1])));
-        const T pz = fma(f.r[6], sp.c[0], fma(f.r[7], sp.c[1], fma(f.r[8], sp.c[2], f.t[2])));
-        T g[3] = {T(0), T(0), T(0)};
-        T d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
-        const bool cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
-        if (cut) d = trunc;
-        d -= offs;  // IneqConst: dist - margin (src/planning.jl:66)
-        dmin = fmin(dmin, d);
-        if (dists) st_soa(dists, sp.out, ldd, off, d);
-        if (GRAD) {
-            const int64_t r0 = (int64_t)sp.out * ndof;
-            uint64_t zm = P.zmask;  // q columns that cannot move this chain: 0
-            while (zm) {
-                const int c = __builtin_ctzll(zm);
-                zm &= zm - 1;
-                st_soa(grads, r0 + c, ldg, off, T(0));
-            }
-            // column j = g . (z_j x (p - o_j)) = z_j . (p x g) - g . m_j with m_j = z_j x o_j
-            // precomputed per configuration (k_coll), so a column costs 6 FMA instead of 12
-            const T w0 = fma(py, g[2], -(pz * g[1])), w1 = fma(pz, g[0], -(px * g[2])), w2 = fma(px, g[1], -(py * g[0]));
-#pragma unroll
-            for (int j = 0; j < MAXA; ++j) {
-                if (S[j].flags & SF_REC) {
-                    T v = T(0);
-                    if (j <= s_last && !cut) {
-                        if (S[j].jkind == MOT_PRISM)
-                            v = fma(g[0], rz[j][0], fma(g[1], rz[j][1], g[2] * rz[j][2]));
-                        else
-                            v = fma(rz[j][0], w0, fma(rz[j][1], w1, fma(rz[j][2], w2,
-                                -fma(g[0], rm[j][0], fma(g[1], rm[j][1], g[2] * rm[j][2])))));
-                    }
-                    uint64_t m = S[j].colmask;
-                    while (m) {
-                        const int c = __builtin_ctzll(m);
-                        m &= m - 1;
-                        st_soa(grads, r0 + c, ldg, off, v);
-                    }
-                }
-            }
-            if (P.flags & PF_BASE) {  // base columns [1 0 -y; 0 1 x; 0 0 0] (src/algorithm.jl:98-103)
-                const int64_t b0 = r0 + P.n_jac;
-                st_soa(grads, b0 + 0, ldg, off, cut ? T(0) : g[0]);
-                st_soa(grads, b0 + 1, ldg, off, cut ? T(0) : g[1]);
-                st_soa(grads, b0 + 2, ldg, off, cut ? T(0) : fma(-g[0], py - by, g[1] * (px - bx)));
-            }
-        }
-    }
-}
-
 template <typename T, int MAXA, bool GRAD>
 __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* __restrict__ S,
                                               const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                               const CollArgs a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                               T* __restrict__ dists, int64_t ldd, T* __restrict__ grads,
                                               int64_t ldg, T* __restrict__ min_dist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)n) return;
-    const uint32_t off = i * (uint32_t)sizeof(T);
-    const bool base = (P.flags & PF_BASE) != 0;
-    T bx = T(0), by = T(0), bth = T(0);
-    if (base) {
-        bx = ld_soa(q, P.base_col, ldq, off);
-        by = ld_soa(q, P.base_col + 1, ldq, off);
-        bth = ld_soa(q, P.base_col + 2, ldq, off);
-    }
-    T qa[MAXA];
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        qa[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
-    }
-    Fr<T> f;
-    if (base) base_frame(f, bx, by, bth);
-    else set_identity(f);
-    const T trunc = (T)a.truncation;
-    const T offs = (T)a.offset;
-    T dmin = T(INFINITY);
-    T ro[MAXA][3], rz[MAXA][3];
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {  // records of unused slots are never read
-        ro[s][0] = ro[s][1] = ro[s][2] = T(0);
-        rz[s][0] = rz[s][1] = rz[s][2] = T(0);
-    }
-    const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
-    coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs, ro,
-                                rz, bx, by, off,
-                          dists, ldd, grads, ldg, dmin);
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        step_a(f, S[s], qa[s], ro[s], rz[s]);
-        if (GRAD) {  // m_s = z_s x o_s (held in ro)
-            const T o0 = ro[s][0], o1 = ro[s][1], o2 = ro[s][2];
-            ro[s][0] = fma(rz[s][1], o2, -(rz[s][2] * o1));
-            ro[s][1] = fma(rz[s][2], o0, -(rz[s][0] * o2));
-            ro[s][2] = fma(rz[s][0], o1, -(rz[s][1] * o0));
-        }
-        coll_spheres<T, MAXA, GRAD>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
-                                    offs, ro, rz, bx, by, off,
-                              dists, ldd, grads, ldg, dmin);
-    }
-    if (min_dist) {
-        if (a.accumulate) dmin = fmin(dmin, ld_soa(min_dist, 0, 0, off));
-        st_soa(min_dist, 0, 0, off, dmin);
-    }
+    coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist);
 }
 
 }  // namespace
@@ -216,7 +22,7 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                        const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
-                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st) {
+                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st) {
     for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
         const int64_t c = std::min(kChunk, n - s0);
         const dim3 grid(grid_of(c, 256)), block(256);
@@ -224,6 +30,16 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
         T* dc = dists ? dists + s0 : dists;
         T* gc = grads ? grads + s0 : grads;
         T* mc = min_dist ? min_dist + s0 : min_dist;
+        if (jf && jf->coll[grads ? 1 : 0]) {
+            int64_t cc = c;
+            CollArgs ac = a;
+            void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc,
+                            (void*)&ldd, (void*)&gc, (void*)&ldg, (void*)&mc};
+            const hipError_t e =
+                hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+            if (e != hipSuccess) return e;
+            continue;
+        }
 #define KIN_CO_LAUNCH(MA) \
         hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
 #define KIN_COG_LAUNCH(MA) \
@@ -244,7 +60,7 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,   \
                                        const LaunchGeom&, const CollArgs&, const T*, int64_t, int64_t, T*,    \
-                                       int64_t, T*, int64_t, T*, hipStream_t);
+                                       int64_t, T*, int64_t, T*, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

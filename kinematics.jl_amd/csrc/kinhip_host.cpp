@@ -189,7 +189,7 @@ struct kin_plan {
     // spheres on several chains: one staged program per chain (kin_coll_plan_create)
     std::vector<std::unique_ptr<kin_plan>> parts;
     // host copy of the staged program (plan specialisation, kinhip_jit.cpp)
-    std::vector<unsigned char> h_steps;
+    std::vector<unsigned char> h_steps, h_sph;
     int32_t n_steps = 0;
     JitKernels* jit = nullptr;
     uint32_t jit_mask = 0;
@@ -736,6 +736,7 @@ struct Stager {
                     hs[k].out = spheres[k].out;
                 }
                 const size_t nb = sizeof(TS) * hs.size();
+                P.h_sph.assign((const unsigned char*)hs.data(), (const unsigned char*)hs.data() + nb);
                 hipError_t e2 = hipMalloc(&P.d_sph, nb);
                 if (e2 != hipSuccess) {
                     P.d_sph = nullptr;
@@ -968,10 +969,12 @@ int plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* pos
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_fk<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)q, ldq, n, (float*)poses,
-                             ldp, (float*)jac, ldj, ta, jit_fk(p->jit), (hipStream_t)stream);
+                             ldp, (float*)jac, ldj, ta, jit_fns(p->jit) ? jit_fns(p->jit)->fk : nullptr,
+                             (hipStream_t)stream);
     else
         e = launch_fk<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)q, ldq, n,
-                              (double*)poses, ldp, (double*)jac, ldj, ta, jit_fk(p->jit), (hipStream_t)stream);
+                              (double*)poses, ldp, (double*)jac, ldj, ta,
+                              jit_fns(p->jit) ? jit_fns(p->jit)->fk : nullptr, (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_fk launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }
@@ -995,22 +998,41 @@ int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q, int64_t l
     return plan_run(p, q, ldq, n, poses, ldp, jac, ldj, TileArgs{tile, tsq, tsp, tsj}, stream, "kin_plan_run_tiled");
 }
 
-int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
-    if (!p) return set_error(KIN_E_INVALID, "kin_plan_specialize: null plan");
-    uint32_t applies = p->is_coll ? 0u : KIN_SPEC_FK;
-    if (kernels == 0) kernels = applies;
-    if (kernels & ~applies) return set_error(KIN_E_UNSUPPORTED, "kin_plan_specialize: kernel kind does not apply");
-    if (kernels == 0 || (p->jit_mask & kernels) == kernels) return KIN_OK;
+namespace {
+int specialize_one(kin_plan* p, uint32_t kernels) {
+    if ((p->jit_mask & kernels) == kernels) return KIN_OK;
     kernels |= p->jit_mask;
     JitKernels* k = nullptr;
     const int rc = p->dtype == KIN_F32
                        ? jit_build<float>(p->pf, (const KStep<float>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
-                                          kernels, &k)
+                                          p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, kernels, &k)
                        : jit_build<double>(p->pd, (const KStep<double>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
-                                           kernels, &k);
+                                           p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, kernels, &k);
     if (rc != KIN_OK) return rc;
     jit_destroy(p->jit);
     p->jit = k;
+    p->jit_mask = kernels;
+    return KIN_OK;
+}
+}  // namespace
+
+int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
+    if (!p) return set_error(KIN_E_INVALID, "kin_plan_specialize: null plan");
+    uint32_t applies = 0;
+    if (p->is_coll) {
+        applies = KIN_SPEC_COLL;
+    } else {
+        applies = KIN_SPEC_FK;
+        if (p->ik_ok) applies |= KIN_SPEC_IK;
+        if (p->ik_ok && !p->with_base) applies |= KIN_SPEC_NAKAMURA;
+    }
+    if (kernels == 0) kernels = applies;
+    if (kernels & ~applies) return set_error(KIN_E_UNSUPPORTED, "kin_plan_specialize: kernel kind does not apply");
+    if (p->parts.empty()) return specialize_one(p, kernels);
+    for (auto& part : p->parts) {  // multi-chain collision plans: every chain program
+        const int rc = specialize_one(part.get(), kernels);
+        if (rc != KIN_OK) return rc;
+    }
     p->jit_mask = kernels;
     return KIN_OK;
 }
@@ -1186,11 +1208,12 @@ int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q
         if (s->dtype == KIN_F32)
             e = launch_coll<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
                                    (const KBox<float>*)sdf->d_f32, s->geom, a, (const float*)q, ldq, n, (float*)dists,
-                                   ldd, (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
+                                   ldd, (float*)grads, ldg, (float*)min_dist, jit_fns(s->jit), (hipStream_t)stream);
         else
             e = launch_coll<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
                                     (const KBox<double>*)sdf->d_f64, s->geom, a, (const double*)q, ldq, n,
-                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, (hipStream_t)stream);
+                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, jit_fns(s->jit),
+                                    (hipStream_t)stream);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
     }
     return KIN_OK;
@@ -1262,10 +1285,10 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,
-                                 (float*)q, ldq, n, iters, (float*)err, lde, (hipStream_t)stream);
+                                 (float*)q, ldq, n, iters, (float*)err, lde, jit_fns(p->jit), (hipStream_t)stream);
     else
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
-                                  (double*)q, ldq, n, iters, (double*)err, lde, (hipStream_t)stream);
+                                  (double*)q, ldq, n, iters, (double*)err, lde, jit_fns(p->jit), (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }
@@ -1281,10 +1304,10 @@ int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_nakamura<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)pts, ldpt,
-                                   (float*)q, ldq, n, (hipStream_t)stream);
+                                   (float*)q, ldq, n, jit_fns(p->jit), (hipStream_t)stream);
     else
         e = launch_nakamura<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)pts, ldpt,
-                                    (double*)q, ldq, n, (hipStream_t)stream);
+                                    (double*)q, ldq, n, jit_fns(p->jit), (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_nakamura launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }

@@ -13,8 +13,10 @@ int set_error(int code, const std::string& msg);
 
 // plan specialisation (kinhip_jit.cpp): kernels compiled for one staged program
 struct JitKernels;
+struct JitFns;
 template <typename T>
-int jit_build(const KProg<T>& P, const KStep<T>* steps, int nsteps, int maxA, uint32_t kernels, JitKernels** out);
+int jit_build(const KProg<T>& P, const KStep<T>* steps, int nsteps, int maxA, const void* spheres, int n_sph,
+              uint32_t kernels, JitKernels** out);
 void jit_destroy(JitKernels* k);
-hipFunction_t jit_fk(const JitKernels* k);
+const JitFns* jit_fns(const JitKernels* k);  // null for a null k
 }  // namespace kinhip

@@ -1,428 +1,29 @@
 // kinhip_ik.hip -- k_ik_dls (batched DLS IK with restarts) and k_nakamura.
 // (gfx950 only; shared helpers in kinhip_device.h)
-#include "kinhip_device.h"
+#include "kinhip_ik_dev.h"
 
 namespace kinhip {
 namespace {
 
 // --------------------------------------------------------------------------
-// shared phase-A evaluator for the IK kernels: q per step in registers
+// generic kernels (the staged program is read from device memory)
 // --------------------------------------------------------------------------
-template <typename T, int MAXA>
-__device__ __forceinline__ void chain_records(const KProg<T>& P, const KStep<T>* __restrict__ S,
-                                              const Fr<T>& root, const T (&qs)[MAXA], Fr<T>& L,
-                                              T (&ro)[MAXA][3], T (&rz)[MAXA][3]) {
-    Fr<T> f = root;
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) step_a(f, S[s], qs[s], ro[s], rz[s]);
-    link_frame(L, f, P.last_has_x != 0, P.Xlast);
-}
-
-// Jacobian column of phase-A step s (geometric; zero for non-recorded steps)
-template <typename T, int ROWS>
-__device__ __forceinline__ void jcol(const KStep<T>& st, const T (&o)[3], const T (&z)[3], const Fr<T>& L,
-                                     T (&J)[ROWS]) {
-    const T m = (st.flags & SF_REC) ? T(1) : T(0);
-    if (st.jkind == MOT_PRISM) {
-        J[0] = m * z[0]; J[1] = m * z[1]; J[2] = m * z[2];
-        if constexpr (ROWS == 6) { J[3] = T(0); J[4] = T(0); J[5] = T(0); }
-    } else {
-        const T dx = L.t[0] - o[0], dy = L.t[1] - o[1], dz = L.t[2] - o[2];
-        J[0] = m * fma(z[1], dz, -(z[2] * dy));
-        J[1] = m * fma(z[2], dx, -(z[0] * dz));
-        J[2] = m * fma(z[0], dy, -(z[1] * dx));
-        if constexpr (ROWS == 6) { J[3] = m * z[0]; J[4] = m * z[1]; J[5] = m * z[2]; }
-    }
-}
-
-// world rotation vector w with exp([w]) R = Rt  (log of Rt R^T)
-template <typename T>
-__device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (&w)[3]) {
-    T E[9];  // row-major E = Rt * R^T
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b)
-            E[3 * a + b] = fma(Rt[3 * a], R[3 * b], fma(Rt[3 * a + 1], R[3 * b + 1], Rt[3 * a + 2] * R[3 * b + 2]));
-    const T v0 = T(0.5) * (E[7] - E[5]);
-    const T v1 = T(0.5) * (E[2] - E[6]);
-    const T v2 = T(0.5) * (E[3] - E[1]);
-    const T s = sqrt_t(v0 * v0 + v1 * v1 + v2 * v2);
-    const T c = T(0.5) * (E[0] + E[4] + E[8] - T(1));
-    const T th = atan2_t(s, c);
-    if (s > T(1e-7)) {
-        const T k = th / s;
-        w[0] = v0 * k; w[1] = v1 * k; w[2] = v2 * k;
-    } else if (c > T(0)) {
-        w[0] = v0; w[1] = v1; w[2] = v2;
-    } else {
-        int b = 0;
-        if (E[4] > E[0]) b = 1;
-        if (E[8] > E[4 * b]) b = 2;
-        T a[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) a[k] = T(0.5) * (E[3 * k + b] + E[3 * b + k]);
-        a[b] = T(0.5) * (E[4 * b] + T(1));
-        const T nn = sqrt_t(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) w[k] = a[k] / nn * th;
-    }
-}
-
-template <typename T>
-struct IkArgsT {
-    int32_t max_iters;
-    T lam2, tol_pos, tol_rot, max_step;
-    int32_t attempt_len;  // 0: no restarts
-    int32_t n_attempts;   // 1 + (max_iters - 1) / attempt_len (attempts the sequential schedule reaches)
-    uint64_t seed;
-    int64_t ibase;  // global index of this chunk's first configuration
-};
-
-// restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
-__device__ __forceinline__ double ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col) {
-    const uint64_t key = (uint64_t)i * 131ull + (uint64_t)attempt * 31ull + (uint64_t)col + 1ull;
-    uint64_t z = seed + 0x9E3779B97F4A7C15ull * key + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
-}
-
-// --------------------------------------------------------------------------
-// k_ik_dls: batched damped least squares, dq = J^T (J J^T + lambda^2 I)^-1 e
-//
-// Restart schedule (kin_ik_params): attempt 0 starts from q0 and is checked at
-// iterations 0..L; attempt k >= 1 starts from seeded random angles at
-// iteration kL + 1 and ends at (k+1)L (the last one at max_iters); the answer
-// is the first attempt that converges.  Attempts are independent, so G lanes
-// of one wave share a target and run attempts slot, slot + G, ... side by side
-// (G = 1: the plain sequential loop).  Each lane's arithmetic is exactly the
-// sequential schedule's; a lane stops once a lower attempt of its target has
-// converged, and the lowest converged attempt (else the last one) is written.
-// Small batches (65k targets = one wave per SIMD) gain G x the parallelism.
-// --------------------------------------------------------------------------
-template <typename T, int MAXA>
-__device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S, const IkArgsT<T>& a,
-                                                 const T* __restrict__ q, int64_t ldq, uint32_t off, int64_t gi,
-                                                 int att, T (&qs)[MAXA]) {
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const KStep<T>& st = S[s];
-        const int32_t c = st.qcol;
-        T v = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
-        if (att > 0 && c >= 0) {
-            if (st.flags & SF_REC) {
-                double lo = (double)st.lo, hi = (double)st.hi;
-                if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
-                v = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, c));
-            } else {
-                v = fmin(fmax(v, st.lo), st.hi);  // attempt 0's first step has clamped it
-            }
-        }
-        qs[s] = v;
-    }
-}
-
 #ifndef KINHIP_IK_WAVES
 #define KINHIP_IK_WAVES 1
 #endif
-// Work distribution: wave w owns targets [w*chunk, (w+1)*chunk) and keeps its
-// 64/G lane groups busy: a group whose target is finished (all its lanes done)
-// writes the result and takes the wave's next target at once, so a wave no
-// longer waits for its slowest target before the others move on.  The queue is
-// wave-local (ballot + popcount, no atomics, nothing in memory between launches).
 template <typename T, int MAXA, int ROWS, int G>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_WAVES))) void k_ik_dls(const KProg<T> P, const KStep<T>* __restrict__ S,
-                                                const IkArgsT<T> a, const T* __restrict__ tgt, int64_t ldt,
-                                                T* __restrict__ q, int64_t ldq, int64_t n,
-                                                int32_t* __restrict__ iters, T* __restrict__ err,
-                                                int64_t lde, int64_t chunk) {
-    const int lane = (int)(threadIdx.x & 63u);
-    const int slot = lane % G, grp = lane / G;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t wbeg = wave * chunk, wend = wbeg + chunk < n ? wbeg + chunk : n;
-    int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
-    int64_t i = 0;
-    bool have = false;    // the first pass of the loop hands every group its first target
-    const bool base = (P.flags & PF_BASE) != 0;
-    const int L = a.attempt_len;
-    const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << (grp * G));
-
-    T Rt[9], pt[3], b0[3], qs[MAXA], b[3];
-    int att = 0, it = 0, res_att = INT_MAX;
-    bool done = true, final_lane = false;
-    uint32_t off = 0;
-    T ep = 0, er = 0;
-    auto start_target = [&]() {
-        off = (uint32_t)i * (uint32_t)sizeof(T);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
-            pt[r] = ld_soa(tgt, 9 + r, ldt, off);
-        }
-        b0[0] = b0[1] = b0[2] = T(0);
-        if (base)
-            for (int k = 0; k < 3; ++k) b0[k] = ld_soa(q, P.base_col + k, ldq, off);
-        b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
-        att = slot;
-        done = att >= a.n_attempts;
-        res_att = INT_MAX;
-        final_lane = false;
-        it = att > 0 ? att * L + 1 : 0;
-        ep = er = T(0);
-        ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
-    };
-    T ro[MAXA][3], rz[MAXA][3];
-    for (;;) {
-        int gm = res_att;  // lowest converged attempt of this lane group's target so far
-        if constexpr (G > 1) {
-#pragma unroll
-            for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
-            if (have && !done && gm < att) done = true;
-        }
-        // a group whose lanes are all done writes its target and takes the next one
-        const uint64_t dmask = __ballot(!have || done);
-        const bool gfin = have && (dmask & gmask) == gmask;
-        if (gfin) {
-            const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
-            if (writer) {
-#pragma unroll
-                for (int s2 = 0; s2 < MAXA; ++s2) {
-                    const int32_t c = S[s2].qcol;
-                    if (c >= 0) st_soa(q, c, ldq, off, qs[s2]);
-                }
-                if (base)
-                    for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
-                if (iters) iters[i] = it;
-                if (err) {
-                    st_soa(err, 0, lde, off, ep);
-                    st_soa(err, 1, lde, off, er);
-                }
-            }
-            have = false;
-        }
-        const uint64_t need = __ballot(!have && slot == 0) & ~0ull;  // group leaders asking for work
-        if (need && next < wend) {
-            const uint64_t lead = 1ull << (grp * G);
-            const int rank = __popcll(need & (lead - 1ull));
-            if (!have && (need & lead) && next + rank < wend) {
-                i = next + rank;
-                have = true;
-                start_target();  // the single (inlined) initialisation site
-            }
-            next += __popcll(need);
-        }
-        if (__ballot(have) == 0) break;  // wave-uniform exit: range drained, every target written
-        if (!have || done) continue;
-        Fr<T> root, L_;
-        if (base) base_frame(root, b[0], b[1], b[2]);
-        else set_identity(root);
-        chain_records<T, MAXA>(P, S, root, qs, L_, ro, rz);
-        const Fr<T>& Lf = L_;
-        T e[6];
-        e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
-        ep = sqrt_t(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
-        er = T(0);
-        if constexpr (ROWS == 6) {
-            T w[3];
-            rot_error(Rt, Lf.r, w);
-            e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
-            er = sqrt_t(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-        }
-        if (ep < a.tol_pos && er < a.tol_rot) {
-            res_att = att;
-            done = true;
-            continue;
-        }
-        if (it >= a.max_iters) {  // only the last attempt gets here
-            final_lane = true;
-            done = true;
-            continue;
-        }
-        if (L > 0 && it > 0 && it % L == 0) {  // attempt over: this lane's next one, if any
-            att += G;
-            if (att >= a.n_attempts) {
-                done = true;
-            } else {
-                it = att * L + 1;
-                ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
-                b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
-            }
-            continue;
-        }
-
-        T Jb[3][ROWS];
-        if (base) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) Jb[k][r] = T(0);
-            Jb[0][0] = T(1);
-            Jb[1][1] = T(1);
-            Jb[2][0] = -(Lf.t[1] - b[1]);
-            Jb[2][1] = Lf.t[0] - b[0];
-            if constexpr (ROWS == 6) Jb[2][5] = T(1);
-        }
-        // pass 0: every joint; pass 1 (lanes that need it): joints sitting on a
-        // limit that the step pushes further out get weight 0 and the system is
-        // re-solved (same rule as the oracle's or_ik_dls_batch)
-        T w[MAXA];
-#pragma unroll
-        for (int s = 0; s < MAXA; ++s) w[s] = T(1);
-        T dq[MAXA], db[3] = {T(0), T(0), T(0)};
-        T mx = T(0);
-        for (int pass = 0; pass < 2; ++pass) {
-            // A = J W J^T + lambda^2 I  (lower triangle)
-            T A[ROWS][ROWS];
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r)
-#pragma unroll
-                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? a.lam2 : T(0);
-#pragma unroll
-            for (int s = 0; s < MAXA; ++s) {
-                T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) J[r] *= w[s];
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r)
-#pragma unroll
-                    for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
-            }
-            if (base) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k)
-#pragma unroll
-                    for (int r = 0; r < ROWS; ++r)
-#pragma unroll
-                        for (int c = 0; c <= r; ++c) A[r][c] = fma(Jb[k][r], Jb[k][c], A[r][c]);
-            }
-            // Cholesky A = L L^T (in place, lower), then y = A^-1 e
-#pragma unroll
-            for (int j = 0; j < ROWS; ++j) {
-                T d = A[j][j];
-#pragma unroll
-                for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
-                d = sqrt_t(d);
-                A[j][j] = d;
-#pragma unroll
-                for (int r = j + 1; r < ROWS; ++r) {
-                    T sm = A[r][j];
-#pragma unroll
-                    for (int k = 0; k < j; ++k) sm -= A[r][k] * A[j][k];
-                    A[r][j] = sm / d;
-                }
-            }
-            T y[ROWS];
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r) {
-                T sm = e[r];
-#pragma unroll
-                for (int k = 0; k < r; ++k) sm -= A[r][k] * y[k];
-                y[r] = sm / A[r][r];
-            }
-#pragma unroll
-            for (int r = ROWS - 1; r >= 0; --r) {
-                T sm = y[r];
-#pragma unroll
-                for (int k = r + 1; k < ROWS; ++k) sm -= A[k][r] * y[k];
-                y[r] = sm / A[r][r];
-            }
-            bool blocked = false;
-            mx = T(0);
-#pragma unroll
-            for (int s = 0; s < MAXA; ++s) {
-                T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
-                T v = T(0);
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
-                v *= w[s];
-                dq[s] = v;
-                if ((qs[s] <= S[s].lo && v < T(0)) || (qs[s] >= S[s].hi && v > T(0))) {
-                    blocked = true;
-                    w[s] = T(0);
-                }
-                mx = fmax(mx, fabs(v));
-            }
-            if (base) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    T v = T(0);
-#pragma unroll
-                    for (int r = 0; r < ROWS; ++r) v = fma(Jb[k][r], y[r], v);
-                    db[k] = v;
-                    mx = fmax(mx, fabs(v));
-                }
-            }
-            if (!blocked) break;
-        }
-        const T sc = mx > a.max_step ? a.max_step / mx : T(1);
-#pragma unroll
-        for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(qs[s] + sc * dq[s], S[s].lo), S[s].hi);
-        if (base)
-            for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
-        ++it;
-    }
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KINHIP_IK_WAVES))) void k_ik_dls(
+    const KProg<T> P, const KStep<T>* __restrict__ S, const IkArgsT<T> a, const T* __restrict__ tgt, int64_t ldt,
+    T* __restrict__ q, int64_t ldq, int64_t n, int32_t* __restrict__ iters, T* __restrict__ err, int64_t lde,
+    int64_t chunk) {
+    ik_body<T, MAXA, ROWS, G>(P, S, a, tgt, ldt, q, ldq, n, iters, err, lde, chunk);
 }
 
-// --------------------------------------------------------------------------
-// k_nakamura: point_inverse_kinematics_nakamura, 50 iterations
-// --------------------------------------------------------------------------
 template <typename T, int MAXA>
 __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                   const T* __restrict__ pts, int64_t ldpt, T* __restrict__ q,
                                                   int64_t ldq, int64_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)n) return;
-    const uint32_t off = i * (uint32_t)sizeof(T);
-    const T pd0 = ld_soa(pts, 0, ldpt, off), pd1 = ld_soa(pts, 1, ldpt, off), pd2 = ld_soa(pts, 2, ldpt, off);
-    T qs[MAXA];
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        qs[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
-    }
-    Fr<T> root;
-    set_identity(root);
-    T ro[MAXA][3], rz[MAXA][3];
-    for (int it = 0; it < 50; ++it) {
-        Fr<T> L;
-        chain_records<T, MAXA>(P, S, root, qs, L, ro, rz);
-        T a = 0, b = 0, c = 0, e = 0, f = 0, ii = 0;  // symmetric J J^T entries
-#pragma unroll
-        for (int s = 0; s < MAXA; ++s) {
-            T J[3];
-            jcol<T, 3>(S[s], ro[s], rz[s], L, J);
-            a += J[0] * J[0]; b += J[0] * J[1]; c += J[0] * J[2];
-            e += J[1] * J[1]; f += J[1] * J[2]; ii += J[2] * J[2];
-        }
-        // `jac * transpose(jac) .+ sr_weight`: +1.0 on EVERY entry (reference quirk)
-        a += T(1); b += T(1); c += T(1); e += T(1); f += T(1); ii += T(1);
-        const T d = b, g = c, h = f;  // symmetric
-        const T A_ = e * ii - f * h, B_ = -(d * ii - f * g), C_ = d * h - e * g;
-        const T det = a * A_ + b * B_ + c * C_;
-        const T i00 = A_ / det, i01 = -(b * ii - c * h) / det, i02 = (b * f - c * e) / det;
-        const T i10 = B_ / det, i11 = (a * ii - c * g) / det, i12 = -(a * f - c * d) / det;
-        const T i20 = C_ / det, i21 = -(a * h - b * g) / det, i22 = (a * e - b * d) / det;
-        const T dp0 = pd0 - L.t[0], dp1 = pd1 - L.t[1], dp2 = pd2 - L.t[2];
-        const T y0 = i00 * dp0 + i01 * dp1 + i02 * dp2;
-        const T y1 = i10 * dp0 + i11 * dp1 + i12 * dp2;
-        const T y2 = i20 * dp0 + i21 * dp1 + i22 * dp2;
-#pragma unroll
-        for (int s = 0; s < MAXA; ++s) {
-            T J[3];
-            jcol<T, 3>(S[s], ro[s], rz[s], L, J);
-            qs[s] += J[0] * y0 + J[1] * y1 + J[2] * y2;
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        if (c >= 0) st_soa(q, c, ldq, off, qs[s]);
-    }
+    nakamura_body<T, MAXA>(P, S, pts, ldpt, q, ldq, n);
 }
 
 }  // namespace
@@ -445,7 +46,7 @@ static int ik_group(int64_t n, int n_attempts, int lanes) {
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, hipStream_t st) {
+                         int64_t lde, const JitFns* jf, hipStream_t st) {
     const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
     const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
@@ -478,6 +79,15 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
+        const hipFunction_t jk = jf ? jf->ik[a.with_rot ? 1 : 0][G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3] : nullptr;
+        if (jk) {
+            int64_t cc = c, pw = per_wave;
+            void* args[] = {(void*)&at, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
+                            (void*)&ic, (void*)&ec, (void*)&lde, (void*)&pw};
+            const hipError_t e = hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+            if (e != hipSuccess) return e;
+            continue;
+        }
 #define KIN_IK_G(MA, R, GG) \
         hipLaunchKernelGGL((k_ik_dls<T, MA, R, GG>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde, per_wave)
 #define KIN_IK6(MA) \
@@ -502,12 +112,19 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
-                           int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st) {
+                           int64_t ldpt, T* q, int64_t ldq, int64_t n, const JitFns* jf, hipStream_t st) {
     for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
         const int64_t c = std::min(kChunk, n - s0);
         const dim3 grid(grid_of(c, 256)), block(256);
         const T* pc = pts + s0;
         T* qc = q + s0;
+        if (jf && jf->nakamura) {
+            int64_t cc = c;
+            void* args[] = {(void*)&pc, (void*)&ldpt, (void*)&qc, (void*)&ldq, (void*)&cc};
+            const hipError_t e = hipModuleLaunchKernel(jf->nakamura, grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+            if (e != hipSuccess) return e;
+            continue;
+        }
 #define KIN_NK_LAUNCH(MA) hipLaunchKernelGGL((k_nakamura<T, MA>), grid, block, 0, st, P, steps, pc, ldpt, qc, ldq, c)
         KIN_MAXA_DISPATCH(g.maxA, KIN_NK_LAUNCH)
 #undef KIN_NK_LAUNCH
@@ -520,9 +137,9 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, \
                                          const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,     \
-                                         hipStream_t);                                                        \
+                                         const JitFns*, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
-                                           int64_t, T*, int64_t, int64_t, hipStream_t);
+                                           int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

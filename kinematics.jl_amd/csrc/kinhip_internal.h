@@ -23,6 +23,15 @@ struct TileArgs {
 };
 inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0}; }
 
+// Plan-specialised kernels of one plan (kinhip_jit.cpp); a null entry means
+// the generic kernel runs.
+struct JitFns {
+    hipFunction_t fk = nullptr;
+    hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
+    hipFunction_t nakamura = nullptr;
+    hipFunction_t coll[2] = {};   // [with gradients]
+};
+
 // jit: the plan-specialised kernel (kinhip_jit.cpp) or null for the generic one
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
@@ -41,24 +50,17 @@ struct IkArgs {
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, hipStream_t st);
+                         int64_t lde, const JitFns* jf, hipStream_t st);
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
-                           int64_t ldpt, T* q, int64_t ldq, int64_t n, hipStream_t st);
+                           int64_t ldpt, T* q, int64_t ldq, int64_t n, const JitFns* jf, hipStream_t st);
 
-struct CollArgs {
-    double truncation;
-    double offset;    // subtracted from every reported distance (IneqConst margin)
-    int32_t n_boxes;  // KBox array (sorted: the first n_aabb are axis-aligned)
-    int32_t n_aabb;   // KAabb array placed right after the KBox array
-    int32_t accumulate;  // min_dist = min(min_dist, this launch's minimum) (multi-chain plans)
-};
 
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                        const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
-                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st);
+                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st);
 
 template <typename T>
 hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,

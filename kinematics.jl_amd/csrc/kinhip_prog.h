@@ -94,6 +94,14 @@ struct Tiling {
     int64_t tsq, tsp, tsj;
 };
 
+struct CollArgs {
+    double truncation;
+    double offset;    // subtracted from every reported distance (IneqConst margin)
+    int32_t n_boxes;  // KBox array (sorted: the first n_aabb are axis-aligned)
+    int32_t n_aabb;   // KAabb array placed right after the KBox array
+    int32_t accumulate;  // min_dist = min(min_dist, this launch's minimum) (multi-chain plans)
+};
+
 template <typename T>
 struct KProg {
     int32_t nA;        // phase-A steps (root -> spine link, padded to the kernel's MAXA)

@@ -5,7 +5,7 @@ Python host mirror of the reference's API over the C-ABI library
 engine only; importing this package on a machine without the built library
 fails loudly.
 """
-from ._lib import KIN_SPEC_FK, KinError, LIB_PATH, lib  # noqa: F401
+from ._lib import KIN_SPEC_COLL, KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_NAKAMURA, KinError, LIB_PATH, lib  # noqa: F401
 from .mechanism import (  # noqa: F401
     BoxMetaData, Joint, Link, Mechanism, Plan, SphereMetaData, Transform, add_new_link, child_joints, child_link,
     child_links, find_joint, find_link, get_jacobian, get_jacobian_, get_jacobian_batch, get_joint_angles,

@@ -22,7 +22,7 @@ KIN_E_UNSUPPORTED, KIN_E_NOMEM, KIN_E_PARSE, KIN_E_IO = -5, -6, -7, -8
 KIN_F32, KIN_F64 = 0, 1
 KIN_JOINT_FIXED, KIN_JOINT_REVOLUTE, KIN_JOINT_PRISMATIC = 0, 1, 2
 KIN_WITH_ROT, KIN_RPY_JAC, KIN_ZERO_FILL = 1, 2, 4
-KIN_SPEC_FK = 1
+KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_NAKAMURA, KIN_SPEC_COLL = 1, 2, 4, 8
 
 # every entry point include/kinhip.h declares (checked by tests/test_abi.py)
 EXPORTS = [

@@ -109,6 +109,17 @@ class CollisionPlan:
             K._lib.kin_plan_destroy(self._h)
             self._h = None
 
+    def specialize(self) -> "CollisionPlan":
+        """kin_plan_specialize(KIN_SPEC_COLL): chain + spheres compiled as constants (boxes stay data)."""
+        K.check(K.lib().kin_plan_specialize(self._h, K.KIN_SPEC_COLL))
+        return self
+
+    @property
+    def specialized(self) -> int:
+        v = C.c_uint32()
+        K.check(K.lib().kin_plan_specialized(self._h, C.byref(v)))
+        return v.value
+
     def run(self, sdf: UnionSDF, Q: torch.Tensor, dists=True, grads=False, min_dist=False,
             truncation=float("inf"), stream=None):
         """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async.

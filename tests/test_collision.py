@@ -266,3 +266,36 @@ def test_gpu_collision_multi_chain(dtype):
     assert not np.any(gd[:14, 8:]) and not np.any(gd[14:, 1:8])  # arm spheres vs head joints and vice versa
     V, Jv = kinhip.IneqConst(sscc, joints, sdf, 1, 0.03, dtype=dtype).eval_batch(Q)
     np.testing.assert_allclose(V.double().cpu().numpy(), np.minimum(rd, 0.08) - 0.03, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_gpu_collision_specialized_equals_generic(dtype, with_base):
+    """KIN_SPEC_COLL (chain + spheres as constants, boxes as data) == the generic k_coll for
+    distances, gradients, minimum, truncation and the IneqConst margin; multi-chain plans too."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(with_base)
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=(1.2, 0.0, 0.0))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    N = 2000
+    g = torch.Generator().manual_seed(6)
+    nq = 8 + (3 if with_base else 0)
+    Q = (torch.rand((nq, N), generator=g, dtype=torch.float64) * 3 - 1.5).to(dtype).to(dev)
+    gen = sscc.plan(arm, dtype=dtype)
+    spe = sscc.plan(arm, dtype=dtype).specialize()
+    assert spe.specialized == kinhip.KIN_SPEC_COLL
+    for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True),
+               dict(dists=True, grads=True, truncation=0.1)):
+        for x, y in zip(gen.run(sdf, Q, **kw), spe.run(sdf, Q, **kw)):
+            assert (x is None and y is None) or torch.equal(x, y), kw
+    if not with_base:  # two chains (arm + head)
+        sscc.add_coll_sphere(m.find_link("head_pan_link"), (0.05, 0.0, 0.1), 0.12)
+        joints = arm + [m.find_joint("head_pan_joint"), m.find_joint("head_tilt_joint")]
+        Q2 = (torch.rand((10, N), generator=g, dtype=torch.float64) * 2 - 1).to(dtype).to(dev)
+        a = sscc.plan(joints, dtype=dtype).run(sdf, Q2, grads=True, min_dist=True)
+        b = sscc.plan(joints, dtype=dtype).specialize().run(sdf, Q2, grads=True, min_dist=True)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)

@@ -256,8 +256,11 @@ def test_specialized_fk_equals_generic(dev, fetch_tree, dtype, with_base, rpy_ja
     gen = m.plan(arm, out_links=links, jac_link=gl, rpy_jac=rpy_jac, dtype=dtype)
     spe = m.plan(arm, out_links=links, jac_link=gl, rpy_jac=rpy_jac, dtype=dtype)
     assert spe.specialized == 0
-    spe.specialize()
+    spe.specialize(kinhip.KIN_SPEC_FK)
     assert spe.specialized == kinhip.KIN_SPEC_FK
+    spe.specialize()  # every kind that applies (+ IK without rpy rows) keeps FK
+    assert spe.specialized & kinhip.KIN_SPEC_FK
+    assert bool(spe.specialized & kinhip.KIN_SPEC_IK) == (not rpy_jac)
     P0, J0 = gen.run(Q)
     P1, J1 = spe.run(Q)
     assert torch.equal(P0, P1) and torch.equal(J0, J1)
@@ -485,3 +488,60 @@ def test_ik_reference_target(dev):
         Tn = kinhip.get_transform(m, gl)
         np.testing.assert_allclose(Tn[:3, 3], T[:3, 3], atol=1e-3)
         np.testing.assert_allclose(kinhip.rpy(Tn), kinhip.rpy(T), atol=1e-3)
+
+
+# ------------------------------------------------------- plan specialisation ---
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_specialized_ik_equals_generic(dev, fetch_tree, dtype, with_base):
+    """KIN_SPEC_IK: specialised k_ik_dls == generic for every lane count, with_rot 0/1, the work-queue
+    schedule and a base; and the specialised Nakamura kernel == generic."""
+    m, arm = _fetch(with_base)
+    gl = m.find_link("gripper_link")
+    om = O.OracleMech(fetch_tree)
+    N = 1500
+    tgt = _targets(om, [j.id for j in arm], gl.id, N, 44)
+    T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
+    gen = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    spe = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype).specialize(kinhip.KIN_SPEC_IK)
+    assert spe.specialized == kinhip.KIN_SPEC_IK
+    nq = 8 + (3 if with_base else 0)
+    for with_rot in (True, False):
+        for lanes in (1, 2, 4, 8):
+            kw = dict(max_iters=23, restarts=3, seed=9, lam=1e-2, max_step=0.5, lanes=lanes, with_rot=with_rot)
+            a = gen.ik_dls(T, torch.zeros((nq, N), dtype=dtype, device=dev), **kw)
+            b = spe.ik_dls(T, torch.zeros((nq, N), dtype=dtype, device=dev), **kw)
+            # angles and iteration counts identical; the reported residual norms may differ in the
+            # last bit (the compilers may contract |e|'s sum of squares differently)
+            assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), (with_rot, lanes)
+            torch.testing.assert_close(a[2], b[2], rtol=1e-5 if dtype == torch.float32 else 1e-12, atol=0)
+    if not with_base:
+        gn = m.plan(arm, jac_link=gl, jac_joints=arm, with_rot=False, dtype=dtype)
+        sn = m.plan(arm, jac_link=gl, jac_joints=arm, with_rot=False, dtype=dtype).specialize(
+            kinhip.KIN_SPEC_NAKAMURA)
+        pts = T[9:12].contiguous()
+        q0 = _rand_q(N, 8, 2, dtype, dev, -0.5, 0.5)
+        a = gn.point_ik_nakamura(pts, q0.clone())
+        b = sn.point_ik_nakamura(pts, q0.clone())
+        # 50 fixed iterations amplify last-bit differences of the two compilations: compare at the
+        # fp64 parity tolerance used against the oracle (test_nakamura_vs_oracle), fp32 by residual
+        if dtype == torch.float64:
+            torch.testing.assert_close(a, b, atol=1e-7, rtol=0)
+        else:
+            pa = gen.run(a)[0][0][9:12]
+            pb = gen.run(b)[0][0][9:12]
+            ra, rb = (pa - pts).norm(dim=0).median(), (pb - pts).norm(dim=0).median()
+            assert float(rb) < 2 * float(ra) + 1e-5
+
+
+def test_specialize_errors(dev):
+    """Kernel kinds that do not apply to a plan are refused (the plan keeps its generic kernels)."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    p = m.plan(arm, out_links=[gl], dtype=torch.float32)  # no Jacobian: no IK
+    with pytest.raises(kinhip.KinError):
+        p.specialize(kinhip.KIN_SPEC_IK)
+    with pytest.raises(kinhip.KinError):
+        p.specialize(kinhip.KIN_SPEC_COLL)
+    assert p.specialized == 0
+    assert p.specialize().specialized == kinhip.KIN_SPEC_FK
