@@ -377,7 +377,7 @@ def main():
                    "parallelism": f"dp{ws} (independent shards)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "kinhip_jit_fk (k_fk body specialised to the Fetch plan)" if args.spec else
+                     "kernel": "kinhip_jit_fk_f32_<program hash> (k_fk body specialised to the plan)" if args.spec else
                      "k_fk<float, 8>", "algorithmic_bytes_per_eval": bytes_per_eval,
                      "avg_launch_us": t_launch * 1e6},
     }
@@ -390,7 +390,7 @@ def main():
         out["config"]["layout"] = f"plain SoA (kin_plan_run), rows padded to ld = N + {args.row_pad}"
     if args.extras:
         out["roofline"]["measured_copy_GBs"] = _copy_bw(dev)
-    if args.extras:
+    if args.sweep:
         # the same workload in the other layouts: plain SoA (padded and unpadded rows), other tiles
         lay = {}
         for name in ("soa_pad%d" % args.row_pad, "soa_pad0", "tile2048", "tile4096", "tile8192",

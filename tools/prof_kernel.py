@@ -13,15 +13,19 @@ sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--what", default="fkjac32", choices=["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fkjac32s", "fkjac32ts", "fkjac64ts", "fk6_64", "ik32", "ik64", "coll32", "collg32", "coll64"])
+BASE = ["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "fk6_64t", "ik32", "ik64", "coll32", "collg32", "coll64"]
+ap.add_argument("--what", default="fkjac32", choices=BASE + [w + "s" for w in BASE],
+                help="workload; a trailing 's' runs the plan-specialised kernels (kin_plan_specialize)")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--n", type=int, default=1 << 20)
 ap.add_argument("--pad", type=int, default=256, help="row padding of the SoA buffers (as bench.py)")
 ap.add_argument("--tile", type=int, default=8192, help="tile of the tiled-SoA workloads (*t, as bench.py)")
 a = ap.parse_args()
-SPEC = a.what.endswith("s") and a.what.startswith("fk")  # plan-specialised kernel (kin_plan_specialize)
+SPEC = a.what.endswith("s")  # plan-specialised kernels (kin_plan_specialize)
 if SPEC:
     a.what = a.what[:-1]
+if a.what.endswith("64t") or a.what.endswith("64"):
+    a.tile = a.tile // 2 if a.what.endswith("t") and a.tile == 8192 else a.tile  # fp64: same bytes per tile row
 if a.what.startswith("ik") and a.n == 1 << 20:
     a.n = 65536  # config 4 size
 dev = torch.device("cuda", 0)
@@ -52,23 +56,35 @@ elif a.what.startswith("fkjac"):
     J = torch.empty((8, 6, ld), dtype=dt, device=dev)[:, :, :a.n]
     for _ in range(a.steps):
         plan.run(Q, P, J)
-elif a.what == "fk6_64":
+elif a.what.startswith("fk6_64"):
     links = [m.find_link(n) for n in ["l_gripper_finger_link", "r_gripper_finger_link", "wrist_flex_link",
                                       "wrist_roll_link", "shoulder_lift_link", "upperarm_roll_link"]]
     plan = m.plan(arm, out_links=links, dtype=dt)
-    P = torch.empty((6, 12, a.n), dtype=dt, device=dev)
-    for _ in range(a.steps):
-        plan.run(Q, P)
+    if SPEC:
+        plan.specialize()
+    if a.what.endswith("t"):
+        Qt = kinhip.tiled(Q, a.tile)
+        P = torch.empty((Qt.shape[0], 6, 12, a.tile), dtype=dt, device=dev)
+        for _ in range(a.steps):
+            plan.run_tiled(Qt, a.n, P)
+    else:
+        P = torch.empty((6, 12, a.n), dtype=dt, device=dev)
+        for _ in range(a.steps):
+            plan.run(Q, P)
 elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge scene
     fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
     sdf = kinhip.fridge_sdf(fr)
     sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
     cp = sscc.plan(arm, dtype=dt)
+    if SPEC:
+        cp.specialize()
     grads = a.what.startswith("collg")
     for _ in range(a.steps):
         cp.run(sdf, Q, dists=grads, grads=grads, min_dist=not grads)
 else:
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if SPEC:
+        plan.specialize()
     T, _ = plan.run(Q)
     tgt = T[0].contiguous()
     for _ in range(a.steps):

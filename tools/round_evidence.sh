@@ -9,8 +9,5 @@ timeout -k 10 600 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/
 cat gpurun_out/bench_default.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/bench -o bench -- python3 bench.py --no-cpu > gpurun_out/bench_rocprof.log 2>&1 || { tail gpurun_out/bench_rocprof.log; exit 4; }
 tail -1 gpurun_out/bench_rocprof.log
-bash tools/prof_session.sh fkjac32 || exit 5
-bash tools/prof_session.sh fkjac64 || exit 6
-bash tools/prof_session.sh coll32 || exit 7
-bash tools/prof_session.sh collg32 || exit 8
+for w in fkjac32ts fkjac64ts fk6_64ts ik32s coll32s collg32s; do bash tools/prof_session.sh $w || exit 5; done
 timeout -k 10 600 python bench.py --no-cpu --sweep --steps 20 > gpurun_out/bench_sweep.json 2> gpurun_out/bench_sweep.err || { tail gpurun_out/bench_sweep.err; exit 9; }

@@ -23,12 +23,20 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "fkjac32t": ("k_fk<float, 8>", (8 + 12 + 48) * 4 * (1 << 20),
                  "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile as run), generic kernel"),
     "fkjac64t": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile 4096)"),
-    "fkjac32s": ("kinhip_jit_fk", (8 + 12 + 48) * 4 * (1 << 20),
+    "fkjac32s": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
                  "FK + 6x8 J, fp32, N = 2^20, plain SoA rows padded by 256, plan-specialised kernel"),
-    "fkjac32ts": ("kinhip_jit_fk", (8 + 12 + 48) * 4 * (1 << 20),
+    "fkjac32ts": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
                   "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile 8192), plan-specialised kernel (bench headline)"),
-    "fkjac64ts": ("kinhip_jit_fk", (8 + 12 + 48) * 8 * (1 << 20),
+    "fkjac64ts": ("kinhip_jit_fk_f64", (8 + 12 + 48) * 8 * (1 << 20),
                   "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile as run), plan-specialised kernel"),
+    "fk6_64ts": ("kinhip_jit_fk_f64", (8 + 72) * 8 * (1 << 20),
+                 "FK of 6 links (config 2), fp64, N = 2^20, tiled SoA (tile 4096), plan-specialised kernel"),
+    "ik32s": ("kinhip_jit_ik_6_4_f32", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
+              "config 4: DLS IK, 65,536 targets, 64 iterations, 3 restarts, G = 4, fp32, plan-specialised kernel"),
+    "coll32s": ("kinhip_jit_coll_0_f32", (8 + 1) * 4 * (1 << 20),
+                "config 5 validity: FK + 14 spheres vs 7-box fridge SDF, min distance, fp32, N = 2^20, specialised"),
+    "collg32s": ("kinhip_jit_coll_1_f32", (8 + 14 + 14 * 8) * 4 * (1 << 20),
+                 "config 5 / IneqConst: 14 distances + 14x8 gradients, fp32, N = 2^20, specialised"),
     "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
     "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
     "ik32": ("k_ik_dls<float, 8, 6, 4>", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
@@ -110,7 +118,7 @@ def main():
     b = os.path.join(PROF, "bench", "bench_kernel_stats.csv")
     if os.path.exists(b):
         shutil.copy(b, os.path.join(OUT, f"{a.round}_bench_kernel_stats.csv"))
-        print("bench:", stats(b, "kinhip_jit_fk"))
+        print("bench:", stats(b, "kinhip_jit_fk_f32"))
 
 
 if __name__ == "__main__":
