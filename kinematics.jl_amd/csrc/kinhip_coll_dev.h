@@ -106,9 +106,10 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
     for (int k = k0; k < k1; ++k) {
         const KSphere<T>& sp = sph[k];
-        const T px = fma(f.r[0], sp.c[0], fma(f.r[1], sp.c[1], fma(f.r[2], sp.c[2], f.t[0])));
-        const T py = fma(f.r[3], sp.c[0], fma(f.r[4], sp.c[1], fma(f.r[5], sp.c[2], f.t[1])));
-        const T pz = fma(f.r[6], sp.c[0], fma(f.r[7], sp.c[1], fma(f.r[8], sp.c[2], f.t[2])));
+        // (fmz: in specialised kernels the sphere's centre is a constant, often with zero components)
+        const T px = fmz(f.r[0], sp.c[0], fmz(f.r[1], sp.c[1], fmz(f.r[2], sp.c[2], f.t[0])));
+        const T py = fmz(f.r[3], sp.c[0], fmz(f.r[4], sp.c[1], fmz(f.r[5], sp.c[2], f.t[1])));
+        const T pz = fmz(f.r[6], sp.c[0], fmz(f.r[7], sp.c[1], fmz(f.r[8], sp.c[2], f.t[2])));
         T g[3] = {T(0), T(0), T(0)};
         T d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
         const bool cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)

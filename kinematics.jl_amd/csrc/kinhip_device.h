@@ -115,6 +115,14 @@ __device__ __forceinline__ float atan2_t(float y, float x) { return atan2f(y, x)
 __device__ __forceinline__ double atan2_t(double y, double x) { return atan2(y, x); }
 __device__ __forceinline__ float sqrt_t(float x) { return sqrtf(x); }
 __device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
+// fp32: the hardware approximations (v_sqrt_f32 / v_rsq_f32 / v_rcp_f32, ~1 ulp) instead of
+// the correctly rounded sequences; fp64: the exact operations (the oracle's arithmetic).
+__device__ __forceinline__ float sqrt_fast(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double sqrt_fast(double x) { return sqrt(x); }
+__device__ __forceinline__ float rsqrt_fast(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ double rsqrt_fast(double x) { return 1.0 / sqrt(x); }
+__device__ __forceinline__ float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double rcp_fast(double x) { return 1.0 / x; }
 
 // SoA addressing: element `row` of a [rows][ld] array for this lane.  Each
 // row gets a wave-uniform buffer descriptor (SGPRs: base = row pointer) and

@@ -49,11 +49,13 @@ __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (
     const T v0 = T(0.5) * (E[7] - E[5]);
     const T v1 = T(0.5) * (E[2] - E[6]);
     const T v2 = T(0.5) * (E[3] - E[1]);
-    const T s = sqrt_t(v0 * v0 + v1 * v1 + v2 * v2);
+    const T s = sqrt_fast(v0 * v0 + v1 * v1 + v2 * v2);
     const T c = T(0.5) * (E[0] + E[4] + E[8] - T(1));
     const T th = atan2_t(s, c);
     if (s > T(1e-7)) {
-        const T k = th / s;
+        T k;
+        if constexpr (sizeof(T) == 4) k = th * rcp_fast(s);
+        else k = th / s;
         w[0] = v0 * k; w[1] = v1 * k; w[2] = v2 * k;
     } else if (c > T(0)) {
         w[0] = v0; w[1] = v1; w[2] = v2;
@@ -221,13 +223,13 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         const Fr<T>& Lf = L_;
         T e[6];
         e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
-        ep = sqrt_t(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        ep = sqrt_fast(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
         er = T(0);
         if constexpr (ROWS == 6) {
             T w[3];
             rot_error(Rt, Lf.r, w);
             e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
-            er = sqrt_t(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+            er = sqrt_fast(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
         if (ep < a.tol_pos && er < a.tol_rot) {
             res_att = att;
@@ -297,20 +299,31 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
                         for (int c = 0; c <= r; ++c) A[r][c] = fma(Jb[k][r], Jb[k][c], A[r][c]);
             }
-            // Cholesky A = L L^T (in place, lower), then y = A^-1 e
+            // Cholesky A = L L^T (in place, lower), then y = A^-1 e.  fp32 keeps the
+            // reciprocal square root of each pivot (hardware v_rsq_f32) and multiplies:
+            // the 6 square roots and 27 divisions of the IEEE form are ~10 instructions
+            // each and dominated the iteration.  fp64 keeps the oracle's exact form
+            // (its iterates are compared with or_ik_dls_batch to 1e-7).
+            constexpr bool fast = sizeof(T) == 4;
+            T ip[ROWS];  // 1 / L[j][j] (fp32)
 #pragma unroll
             for (int j = 0; j < ROWS; ++j) {
                 T d = A[j][j];
 #pragma unroll
                 for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
-                d = sqrt_t(d);
-                A[j][j] = d;
+                if constexpr (fast) {
+                    ip[j] = rsqrt_fast(d);
+                } else {
+                    d = sqrt_t(d);
+                    A[j][j] = d;
+                }
 #pragma unroll
                 for (int r = j + 1; r < ROWS; ++r) {
                     T sm = A[r][j];
 #pragma unroll
                     for (int k = 0; k < j; ++k) sm -= A[r][k] * A[j][k];
-                    A[r][j] = sm / d;
+                    if constexpr (fast) A[r][j] = sm * ip[j];
+                    else A[r][j] = sm / d;
                 }
             }
             T y[ROWS];
@@ -319,14 +332,16 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 T sm = e[r];
 #pragma unroll
                 for (int k = 0; k < r; ++k) sm -= A[r][k] * y[k];
-                y[r] = sm / A[r][r];
+                if constexpr (fast) y[r] = sm * ip[r];
+                else y[r] = sm / A[r][r];
             }
 #pragma unroll
             for (int r = ROWS - 1; r >= 0; --r) {
                 T sm = y[r];
 #pragma unroll
                 for (int k = r + 1; k < ROWS; ++k) sm -= A[k][r] * y[k];
-                y[r] = sm / A[r][r];
+                if constexpr (fast) y[r] = sm * ip[r];
+                else y[r] = sm / A[r][r];
             }
             bool blocked = false;
             mx = T(0);
