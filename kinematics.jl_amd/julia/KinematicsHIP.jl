@@ -91,9 +91,10 @@ mutable struct HIPModel
     handle::Ptr{Cvoid}
     m::Mechanism
     plans::Dict{Any,Ptr{Cvoid}}
+    specialize::Bool  # compile every new plan into constant-folded kernels (kin_plan_specialize)
 end
 
-function HIPModel(m::Mechanism)
+function HIPModel(m::Mechanism; specialize::Bool=true)
     J = length(m.joints)
     jt = Int32[joint_type_code(j) for j in m.joints]
     jp = Int32[j.plink_id for j in m.joints]
@@ -113,7 +114,7 @@ function HIPModel(m::Mechanism)
         check(ccall((:kin_model_create, libkinhip), Cint, (Ref{KinTreeDesc}, Ref{Ptr{Cvoid}}), d, h))
     end
     check(ccall((:kin_model_set_angles, libkinhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], m.angles))
-    hm = HIPModel(h[], m, Dict{Any,Ptr{Cvoid}}())
+    hm = HIPModel(h[], m, Dict{Any,Ptr{Cvoid}}(), specialize)
     finalizer(hm) do x
         for p in values(x.plans)
             ccall((:kin_plan_destroy, libkinhip), Cint, (Ptr{Cvoid},), p)
@@ -136,6 +137,8 @@ function plan!(hm::HIPModel, ::Type{T}, qj, outs, jl, jj, flags) where {T}
             check(ccall((:kin_plan_create, libkinhip), Cint, (Ptr{Cvoid}, Ref{KinPlanDesc}, Ref{Ptr{Cvoid}}),
                         hm.handle, d, h))
         end
+        # every kernel kind that applies (0); a failed compilation leaves the generic kernels
+        hm.specialize && ccall((:kin_plan_specialize, libkinhip), Cint, (Ptr{Cvoid}, UInt32), h[], UInt32(0))
         h[]
     end
 end
@@ -167,6 +170,25 @@ function Kinematics.get_jacobian!(hm::HIPModel, link::Link, joints::Vector{<:Joi
                 (Ptr{Cvoid}, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
                 p, pointer(Q), stride(Q, 2), N, pose === nothing ? C_NULL : pointer(pose), N, pointer(J), N,
                 stream_ptr()))
+    J
+end
+
+"""Batched `get_jacobian!` on the tiled layout (kin_plan_run_tiled, DESIGN.md section 3):
+Q is (tile, dof, ntiles), J (tile, rows, cols, ntiles), pose (tile, 12, ntiles) or nothing; N <= tile * ntiles
+configurations, configuration i at [i % tile + 1, ..., i ÷ tile + 1]."""
+function get_jacobian_tiled!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool, J::ROCArray{T,4},
+                             Q::ROCArray{T,3}, N::Integer; rpy_jac=false,
+                             pose::Union{Nothing,ROCArray{T,3}}=nothing) where {T<:Union{Float32,Float64}}
+    tile = size(Q, 1)
+    flags = (with_rot ? KIN_WITH_ROT : UInt32(0)) | (rpy_jac ? KIN_RPY_JAC : UInt32(0))
+    ids = Int32[j.id for j in joints]
+    outs = pose === nothing ? Int32[] : Int32[link.id]
+    p = plan!(hm, T, ids, outs, Int32(link.id), ids, flags)
+    check(ccall((:kin_plan_run_tiled, libkinhip), Cint,
+                (Ptr{Cvoid}, Int64, Ptr{T}, Int64, Int64, Int64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Int64, Ptr{Cvoid}),
+                p, tile, pointer(Q), stride(Q, 2), stride(Q, 3), N,
+                pose === nothing ? C_NULL : pointer(pose), tile, pose === nothing ? 0 : stride(pose, 3),
+                pointer(J), tile, stride(J, 4), stream_ptr()))
     J
 end
 
@@ -254,6 +276,7 @@ function coll_plan!(hm::HIPModel, ::Type{T}, sscc::Kinematics.SweptSphereCollisi
             check(ccall((:kin_coll_plan_create, libkinhip), Cint, (Ptr{Cvoid}, Ref{KinCollDesc}, Ref{Ptr{Cvoid}}),
                         hm.handle, d, h))
         end
+        hm.specialize && ccall((:kin_plan_specialize, libkinhip), Cint, (Ptr{Cvoid}, UInt32), h[], UInt32(0))
         h[]
     end
 end
@@ -303,6 +326,6 @@ function pose_const!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot
     vals, jac
 end
 
-export HIPModel, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
+export HIPModel, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
 
 end # module
