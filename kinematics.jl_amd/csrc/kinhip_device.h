@@ -154,6 +154,27 @@ __device__ __forceinline__ void st_soa(double* __restrict__ base, int64_t row, i
                                           KINHIP_STORE_AUX);
 }
 
+// "Narrow" SoA addressing: one buffer descriptor per array and the row folded into the
+// 32-bit lane offset.  For kernels that touch many rows rarely (IK: 12 target rows, the q
+// rows, 2 error rows) the per-row descriptors of ld_soa are loop-invariant, get hoisted and
+// occupy 4 SGPRs each; with ~30 rows they overflow the SGPR file and spill into VGPR lanes.
+// Valid while rows * ld * sizeof(T) < 2^31 (the launcher checks).
+__device__ __forceinline__ float ldn_soa(const float* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), (int)(off + (uint32_t)(row * ld * 4)), 0, 0));
+}
+__device__ __forceinline__ double ldn_soa(const double* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base),
+                                                                           (int)(off + (uint32_t)(row * ld * 8)), 0, 0));
+}
+__device__ __forceinline__ void stn_soa(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base), (int)(off + (uint32_t)(row * ld * 4)), 0,
+                                          KINHIP_STORE_AUX);
+}
+__device__ __forceinline__ void stn_soa(double* __restrict__ base, int64_t row, int64_t ld, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), row_rsrc(base),
+                                          (int)(off + (uint32_t)(row * ld * 8)), 0, KINHIP_STORE_AUX);
+}
+
 template <typename T>
 __device__ __forceinline__ void set_identity(Fr<T>& f) {
 #pragma unroll
@@ -410,9 +431,5 @@ inline unsigned grid_of(int64_t n, int block) { return (unsigned)((n + block - 1
     default: CALL(32); break;      \
     }
 
-// Launches are split into chunks of kChunk configurations so that every lane
-// byte offset (uint32, ld_soa / st_soa) fits in 32 bits; chunks are pointer
-// offsets into the same SoA arrays (the leading dimensions do not change).
-constexpr int64_t kChunk = int64_t(1) << 27;
 
 }  // namespace kinhip

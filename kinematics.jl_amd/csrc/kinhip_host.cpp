@@ -1282,13 +1282,20 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
         return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
     IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
              prm->restarts, prm->seed, prm->lanes};
+    // the specialised IK kernels address rows with 32-bit offsets (ldn_soa): every lane offset of a
+    // launch chunk plus rows * ld must stay below 2^31 bytes, else the generic kernel runs
+    const int64_t esz = p->dtype == KIN_F32 ? 4 : 8;
+    const int64_t span = std::min<int64_t>(n, kIkChunk);
+    const bool narrow = (12 * ldt + span) * esz < (int64_t(1) << 31) && (p->nqcols * ldq + span) * esz < (int64_t(1) << 31) &&
+                        (2 * lde + span) * esz < (int64_t(1) << 31);
+    const JitFns* jf = narrow ? jit_fns(p->jit) : nullptr;
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,
-                                 (float*)q, ldq, n, iters, (float*)err, lde, jit_fns(p->jit), (hipStream_t)stream);
+                                 (float*)q, ldq, n, iters, (float*)err, lde, jf, (hipStream_t)stream);
     else
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
-                                  (double*)q, ldq, n, iters, (double*)err, lde, jit_fns(p->jit), (hipStream_t)stream);
+                                  (double*)q, ldq, n, iters, (double*)err, lde, jf, (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }

@@ -58,7 +58,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         return (int64_t)(cus > 0 ? cus : 256) * 8;
     }();
-    const int64_t chunk = kChunk / 8;  // lane byte offsets i * sizeof(T) stay below 2^32
+    const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = s0;
         const int64_t c = std::min(chunk, n - s0);

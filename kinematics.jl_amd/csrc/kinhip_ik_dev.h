@@ -7,6 +7,17 @@
 namespace kinhip {
 namespace {
 
+#ifndef KINHIP_IK_NARROW
+#define KINHIP_IK_NARROW 0  // 1: narrow SoA addressing (ldn_soa) in k_ik_dls, see kinhip_device.h
+#endif
+#if KINHIP_IK_NARROW
+#define KIN_IK_LD ldn_soa
+#define KIN_IK_ST stn_soa
+#else
+#define KIN_IK_LD ld_soa
+#define KIN_IK_ST st_soa
+#endif
+
 // --------------------------------------------------------------------------
 // shared phase-A evaluator for the IK kernels: q per step in registers
 // --------------------------------------------------------------------------
@@ -114,7 +125,7 @@ __device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S,
     for (int s = 0; s < MAXA; ++s) {
         const KStep<T>& st = S[s];
         const int32_t c = st.qcol;
-        T v = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
+        T v = c >= 0 ? KIN_IK_LD(q, c, ldq, off) : T(0);
         if (att > 0 && c >= 0) {
             if (st.flags & SF_REC) {
                 double lo = (double)st.lo, hi = (double)st.hi;
@@ -159,12 +170,12 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
-            pt[r] = ld_soa(tgt, 9 + r, ldt, off);
+            for (int c = 0; c < 3; ++c) Rt[3 * r + c] = KIN_IK_LD(tgt, r + 3 * c, ldt, off);
+            pt[r] = KIN_IK_LD(tgt, 9 + r, ldt, off);
         }
         b0[0] = b0[1] = b0[2] = T(0);
         if (base)
-            for (int k = 0; k < 3; ++k) b0[k] = ld_soa(q, P.base_col + k, ldq, off);
+            for (int k = 0; k < 3; ++k) b0[k] = KIN_IK_LD(q, P.base_col + k, ldq, off);
         b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
         att = slot;
         done = att >= a.n_attempts;
@@ -191,14 +202,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
                 for (int s2 = 0; s2 < MAXA; ++s2) {
                     const int32_t c = S[s2].qcol;
-                    if (c >= 0) st_soa(q, c, ldq, off, qs[s2]);
+                    if (c >= 0) KIN_IK_ST(q, c, ldq, off, qs[s2]);
                 }
                 if (base)
-                    for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
+                    for (int k = 0; k < 3; ++k) KIN_IK_ST(q, P.base_col + k, ldq, off, b[k]);
                 if (iters) iters[i] = it;
                 if (err) {
-                    st_soa(err, 0, lde, off, ep);
-                    st_soa(err, 1, lde, off, er);
+                    KIN_IK_ST(err, 0, lde, off, ep);
+                    KIN_IK_ST(err, 1, lde, off, er);
                 }
             }
             have = false;

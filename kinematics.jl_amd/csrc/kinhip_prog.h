@@ -34,6 +34,13 @@ enum : int32_t { SF_REC = 1, SF_HAS_X = 2, SF_SCALE = 4 };
 enum : int32_t { LOAD_NONE = -1, LOAD_ROOT = -2 };
 enum : int32_t { PF_JAC = 1, PF_WITH_ROT = 2, PF_RPY = 4, PF_ZERO = 8, PF_BASE = 16 };
 
+// Launches are split into chunks of kChunk configurations so that every lane
+// byte offset (uint32, ld_soa / st_soa) fits in 32 bits; chunks are pointer
+// offsets into the same SoA arrays (the leading dimensions do not change).
+// The IK kernels take kIkChunk per launch.
+constexpr int64_t kChunk = int64_t(1) << 27;
+constexpr int64_t kIkChunk = kChunk / 8;
+
 constexpr int kMaxChain = 32;  // phase-A steps (root -> spine link), register resident
 constexpr int kMaxJacCols = 64;
 constexpr int kMaxSlots = 8;

@@ -14,8 +14,10 @@ m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
 arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
 gl = m.find_link("gripper_link")
 out = []
-for dt in (torch.float32, torch.float64):
+for dt in ((torch.float32,) if os.environ.get("AB_F32") else (torch.float32, torch.float64)):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
+    if int(os.environ.get("AB_SPEC", "0")):
+        plan.specialize()
     n = int(os.environ.get("IK_N", 65536))
     Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=4242,
                                 dtype=dt, device=dev)
@@ -35,4 +37,5 @@ for dt in (torch.float32, torch.float64):
     out.append(f"{str(dt)[6:]}: {ms:.3f} ms/batch {n / ms * 1e3:.3e} solves/s succ {(it < 64).float().mean():.4f} "
                f"mean_it {it.float().mean():.2f} qsum {float(Q.double().sum()):.6f}")
 print(os.path.basename(os.environ.get("KINHIP_LIB", "default")), "G=" + os.environ.get("KINHIP_IK_GROUP", "auto"),
+      "Q=" + os.environ.get("KINHIP_IK_QUEUE", "auto"), "spec=" + os.environ.get("AB_SPEC", "0"),
       " | ".join(out), flush=True)
