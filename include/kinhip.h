@@ -197,6 +197,10 @@ enum {
 KINHIP_API int kin_plan_specialize(kin_plan* p, uint32_t kernels);
 /* The KIN_SPEC_* mask the plan currently runs specialised. */
 KINHIP_API int kin_plan_specialized(const kin_plan* p, uint32_t* kernels);
+/* Compiles (does not load) a synthetic program with every specialised kernel kind in
+ * both precisions: checks run-time compilation on the host, no GPU needed.  0 = ok;
+ * otherwise kin_last_error() holds the compiler log. */
+KINHIP_API int kin_jit_selfcheck(void);
 
 /* One-shot conveniences with an internal per-model plan cache (the first call
  * for a request stages it synchronously; later calls are async).

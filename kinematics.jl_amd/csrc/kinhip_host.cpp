@@ -1037,6 +1037,8 @@ int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
     return KIN_OK;
 }
 
+int kin_jit_selfcheck(void) { return jit_selfcheck(); }
+
 int kin_plan_specialized(const kin_plan* p, uint32_t* kernels) {
     if (!p || !kernels) return set_error(KIN_E_INVALID, "kin_plan_specialized: null argument");
     *kernels = p->jit_mask;

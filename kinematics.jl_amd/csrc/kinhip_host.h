@@ -19,4 +19,5 @@ int jit_build(const KProg<T>& P, const KStep<T>* steps, int nsteps, int maxA, co
               uint32_t kernels, JitKernels** out);
 void jit_destroy(JitKernels* k);
 const JitFns* jit_fns(const JitKernels* k);  // null for a null k
+int jit_selfcheck();
 }  // namespace kinhip

@@ -33,7 +33,7 @@ EXPORTS = [
     "kin_urdf_link_name", "kin_urdf_joint_name", "kin_urdf_find_link", "kin_urdf_find_joint",
     "kin_urdf_link_box",
     "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run", "kin_plan_run_tiled",
-    "kin_plan_specialize", "kin_plan_specialized",
+    "kin_plan_specialize", "kin_plan_specialized", "kin_jit_selfcheck",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
@@ -112,6 +112,7 @@ def lib():
         "kin_plan_run": ([P, P, I64, I64, P, I64, P, I64, P], C.c_int),
         "kin_plan_specialize": ([P, U32], C.c_int),
         "kin_plan_specialized": ([P, P], C.c_int),
+        "kin_jit_selfcheck": ([], C.c_int),
         "kin_plan_run_tiled": ([P, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P], C.c_int),
         "kin_get_transform_batch": ([P, I32, I32, P, P, I64, I64, I32, P, P, I64, P], C.c_int),
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),
