@@ -52,12 +52,19 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
                   0};
     const int G = ik_group(n, natt, a.lanes);
-    static const int64_t resident_waves = [] {  // 2 waves per SIMD: the IK kernels hold ~190 VGPRs
-        int dev = 0, cus = 0;
+    static const int cus = [] {
+        int dev = 0, c = 0;
         (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return (int64_t)(cus > 0 ? cus : 256) * 8;
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c > 0 ? c : 256;
     }();
+    // waves per CU that stay resident: 2 per SIMD for the generic kernels (~190-240 VGPRs);
+    // KINHIP_IK_RESIDENT=<waves per CU> overrides (A/B)
+    static const int res_env = [] {
+        const char* e = getenv("KINHIP_IK_RESIDENT");
+        return e ? atoi(e) : 0;
+    }();
+    const int64_t resident_waves = (int64_t)cus * (res_env > 0 ? res_env : 8);
     const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = s0;
