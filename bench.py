@@ -460,7 +460,7 @@ def main():
                 "a11_nakamura_f64": _nakamura_leg(m, arm, gl, ctx, stream, spec=0)["value"]}
     if SPEC_ERRORS:
         out["specialization_errors"] = SPEC_ERRORS
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and ws == 1 and not args.no_cpu:  # the CPU baseline is a single-GPU-run figure
         out["cpu_baseline"] = _cpu_baseline(m)
     if rank == 0:
         print(json.dumps(out), flush=True)
