@@ -111,6 +111,12 @@ def test_gpu_random_tree_vs_oracle(tmp_path, seed):
         if dtype == torch.float32:  # sentinel was rounded to fp32 on the device
             rj = np.where(rj == init, init.astype(np.float32).astype(np.float64), rj)
         np.testing.assert_allclose(got, rj, atol=tol, rtol=1e-4 if dtype == torch.float32 else 1e-9)
+        if seed < 24:  # plan specialisation (constant-folded program) == generic kernel, bit for bit
+            spe = m.plan(qj, out_links=[m.links[o - 1] for o in outs], jac_link=m.links[jac_link - 1],
+                         jac_joints=[m.joints[j - 1] for j in jac_ids], with_rot=with_rot, rpy_jac=rpy_jac,
+                         zero_fill=zero_fill, dtype=dtype).specialize(kinhip.KIN_SPEC_FK)
+            P2, J2 = spe.run(Qd, jac=torch.tensor(init, dtype=dtype, device="cuda"))
+            assert torch.equal(P2, P) and torch.equal(J2, Jd)
 
 
 @pytest.mark.gpu
@@ -163,3 +169,7 @@ def test_gpu_random_tree_collision_vs_oracle(tmp_path, seed):
     np.testing.assert_allclose(D.cpu().numpy(), rd, atol=1e-9)
     np.testing.assert_allclose(Mn.cpu().numpy(), rd.min(0), atol=1e-9)
     assert (np.abs(G.cpu().numpy() - rg) > 2e-5 * (1 + np.abs(rg))).mean() < 2e-3
+    # specialised (chain + spheres folded; multi-chain plans specialise every program) == generic
+    spe = sscc.plan([m.joints[j - 1] for j in q_ids], dtype=torch.float64).specialize()
+    for x, y in zip((D, G, Mn), spe.run(sdf, Qd, grads=True, min_dist=True)):
+        assert torch.equal(x, y)
