@@ -192,6 +192,55 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
                 torch.cuda.synchronize()
                 out[name]["gather_ms"] = D.max_over_ranks(ctx, [(time.perf_counter() - g0) * 1e3])[0]
                 assert allv.shape[1] == n * ctx.world
+    # IneqConst (src/planning.jl:55-68) over n waypoints: margin 0.03, truncation margin + 0.05, one
+    # kin_ineq_const_batch launch.  Two inputs: the random samples above, and n / 64 straight-line
+    # trajectories of 64 waypoints each (create_straight_trajectory between random start / goal
+    # configurations, waypoints of one trajectory side by side) -- the planner's workload, where the
+    # broad phase (spheres provably beyond the truncation skip the boxes wave-wide) applies.
+    ic = kinhip.IneqConst(sscc, arm, sdf, 1, 0.03, dtype=dt)
+    if spec:
+        _specialize(ic.plan)
+    lo_ = torch.tensor([j.lower_limit for j in arm], dtype=torch.float64)
+    hi_ = torch.tensor([j.upper_limit for j in arm], dtype=torch.float64)
+    gen = torch.Generator().manual_seed(77 + ctx.rank)
+    nt = n // 64
+    qs = lo_[:, None] + (hi_ - lo_)[:, None] * torch.rand((8, nt), generator=gen, dtype=torch.float64)
+    qg = lo_[:, None] + (hi_ - lo_)[:, None] * torch.rand((8, nt), generator=gen, dtype=torch.float64)
+    tt = torch.linspace(0, 1, 64, dtype=torch.float64)
+    Qtraj = (qs[:, :, None] + (qg - qs)[:, :, None] * tt).reshape(8, nt * 64).to(dt).to(ctx.device).contiguous()
+    ns = plan.n_sph
+    nbytes = 8 * 4 + ns * 4 + ns * 8 * 4
+    tile = 8192
+    Qt_rand, Qt_traj = kinhip.tiled(Q, tile), kinhip.tiled(Qtraj, tile)
+    for name, Qx, run in (("ineq_const_random", Q, lambda: ic.eval_batch(Q, stream=stream)),
+                          ("ineq_const_trajectories", Qtraj, lambda: ic.eval_batch(Qtraj, stream=stream)),
+                          ("ineq_const_trajectories_tiled", Qtraj,
+                           lambda: ic.eval_batch_tiled(Qt_traj, n, stream=stream)),
+                          ("dists_grads_tiled", Q, lambda: plan.run_tiled(sdf, Qt_rand, n, grads=True,
+                                                                          stream=stream))):
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                run()
+        torch.cuda.synchronize()
+        D.barrier(ctx)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        D.barrier(ctx)
+        wall, dev_s = D.max_over_ranks(ctx, [time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3])
+        nx = Qx.shape[1]
+        out[name] = {"value": nx * ctx.world * steps / wall,
+                     "unit": "waypoints/s (values + gradients)" if name.startswith("ineq") else "FK+SDF samples/s",
+                     "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
+                     "achieved_GBs": nbytes * nx / (dev_s / steps) / 1e9}
+        if name.startswith("ineq"):
+            out[name]["margin"] = 0.03
+        if name.endswith("tiled"):
+            out[name]["layout"] = f"tiled SoA, tile {tile}"
     out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
                        f"samples sharded across ranks, {'specialised' if spec else 'generic'} kernels")
     return out
@@ -461,6 +510,7 @@ def main():
                 "ik_dls_1M_targets": _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=0)["value"],
                 "config5_fk_sdf": {k: v["value"] for k, v in _coll_leg(ctx, stream, N, max(5, args.steps // 2),
                                                                         spec=0).items() if isinstance(v, dict)},
+                # (the generic ineq_const figures include the broad phase, which both kernels have)
                 "a11_nakamura_f64": _nakamura_leg(m, arm, gl, ctx, stream, spec=0)["value"]}
     if SPEC_ERRORS:
         out["specialization_errors"] = SPEC_ERRORS

@@ -287,6 +287,14 @@ KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double trun
                               int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
                               void* stream);
 
+/* kin_coll_batch on the tiled layout (see kin_plan_run_tiled): element (config i,
+ * row r) of q / dists / grads / min_dist at X[(i / tile) * ts + r * ld + i % tile]
+ * (min_dist has one row; its ld is 1 element per configuration, ts its tile stride). */
+KINHIP_API int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double truncation, int64_t tile,
+                                    const void* q, int64_t ldq, int64_t tsq, int64_t n, void* dists, int64_t ldd,
+                                    int64_t tsd, void* grads, int64_t ldg, int64_t tsg, void* min_dist, int64_t tsm,
+                                    void* stream);
+
 /* ------------------------------------------------------------------------- */
 /* Planning constraints over waypoints (src/planning.jl) */
 /* ------------------------------------------------------------------------- */
@@ -299,6 +307,10 @@ KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double trun
 KINHIP_API int kin_ineq_const_batch(const kin_plan* coll_plan, const kin_sdf* sdf, double margin, const void* q,
                                     int64_t ldq, int64_t n, void* vals, int64_t ldv, void* jac, int64_t ldj,
                                     void* stream);
+/* kin_ineq_const_batch on the tiled layout (kin_coll_batch_tiled's conventions). */
+KINHIP_API int kin_ineq_const_batch_tiled(const kin_plan* coll_plan, const kin_sdf* sdf, double margin, int64_t tile,
+                                          const void* q, int64_t ldq, int64_t tsq, int64_t n, void* vals, int64_t ldv,
+                                          int64_t tsv, void* jac, int64_t ldj, int64_t tsj, void* stream);
 /* PoseConstraint (src/planning.jl:114-138) of one link for N configurations.
  * `p` must come from kin_plan_create with n_out = 1, jac_link = that link and
  * jac_flags = KIN_RPY_JAC | KIN_WITH_ROT (6 rows) or 0 (position only, 3 rows).

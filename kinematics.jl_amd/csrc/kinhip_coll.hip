@@ -13,8 +13,8 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
                                               const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                               const CollArgs a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                               T* __restrict__ dists, int64_t ldd, T* __restrict__ grads,
-                                              int64_t ldg, T* __restrict__ min_dist) {
-    coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist);
+                                              int64_t ldg, T* __restrict__ min_dist, const Tiling tl) {
+    coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl);
 }
 
 }  // namespace
@@ -22,28 +22,34 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                        const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
-                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st) {
-    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
-        const int64_t c = std::min(kChunk, n - s0);
+                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const TileArgs& ta, const JitFns* jf,
+                       hipStream_t st) {
+    // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
+    const bool tiled = ta.tile < n;
+    const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
+    Tiling tl{tiled ? (uint32_t)(ta.tile / 256) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, ta.tsm};
+    for (int64_t s0 = 0; s0 < n; s0 += chunk) {
+        const int64_t c = std::min(chunk, n - s0);
         const dim3 grid(grid_of(c, 256)), block(256);
-        const T* qc = q + s0;
-        T* dc = dists ? dists + s0 : dists;
-        T* gc = grads ? grads + s0 : grads;
-        T* mc = min_dist ? min_dist + s0 : min_dist;
+        const int64_t nt = tiled ? s0 / ta.tile : 0;
+        const T* qc = q + (tiled ? nt * ta.tsq : s0);
+        T* dc = dists ? dists + (tiled ? nt * ta.tsp : s0) : dists;
+        T* gc = grads ? grads + (tiled ? nt * ta.tsj : s0) : grads;
+        T* mc = min_dist ? min_dist + (tiled ? nt * ta.tsm : s0) : min_dist;
         if (jf && jf->coll[grads ? 1 : 0]) {
             int64_t cc = c;
             CollArgs ac = a;
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc,
-                            (void*)&ldd, (void*)&gc, (void*)&ldg, (void*)&mc};
+                            (void*)&ldd, (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tl};
             const hipError_t e =
                 hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }
 #define KIN_CO_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
+        hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
 #define KIN_COG_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_coll<T, MA, true>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc)
+        hipLaunchKernelGGL((k_coll<T, MA, true>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
         if (grads) {
             KIN_MAXA_DISPATCH(g.maxA, KIN_COG_LAUNCH)
         } else {
@@ -60,7 +66,7 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,   \
                                        const LaunchGeom&, const CollArgs&, const T*, int64_t, int64_t, T*,    \
-                                       int64_t, T*, int64_t, T*, const JitFns*, hipStream_t);
+                                       int64_t, T*, int64_t, T*, const TileArgs&, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

@@ -99,7 +99,7 @@ template <typename T, int MAXA, bool GRAD>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
                                              const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
                                              const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb,
-                                             int na, int nb, T trunc, T offs,
+                                             int na, int nb, T trunc, T offs, bool broad, const T (&bnd)[6],
                                              const T (&rm)[MAXA][3], const T (&rz)[MAXA][3], T bx, T by,
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
                                              T* __restrict__ grads, int64_t ldg, T& dmin) {
@@ -111,9 +111,30 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         const T py = fmz(f.r[3], sp.c[0], fmz(f.r[4], sp.c[1], fmz(f.r[5], sp.c[2], f.t[1])));
         const T pz = fmz(f.r[6], sp.c[0], fmz(f.r[7], sp.c[1], fmz(f.r[8], sp.c[2], f.t[2])));
         T g[3] = {T(0), T(0), T(0)};
-        T d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
-        const bool cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
-        if (cut) d = trunc;
+        // Broad phase (finite truncation only): every box lies inside the world-aligned box
+        // (centre bnd[0..2], half extents bnd[3..5]), so a distance to it beyond trunc + r proves
+        // sdf(p) - r > trunc: the reference would report the truncated value with a zero gradient,
+        // and that is written without evaluating the boxes when the whole wave agrees (wave-uniform
+        // skip; the slack covers rounding of the exact path).  Results are identical to evaluating
+        // every box.
+        bool far = false;
+        if (broad) {
+            const T ox = fmax(fabs(px - bnd[0]) - bnd[3], T(0));
+            const T oy = fmax(fabs(py - bnd[1]) - bnd[4], T(0));
+            const T oz = fmax(fabs(pz - bnd[2]) - bnd[5], T(0));
+            const T lim = fma(trunc + sp.r, T(1.0001), T(1e-5));
+            far = lim > T(0) && fma(ox, ox, fma(oy, oy, oz * oz)) > lim * lim;
+        }
+        T d;
+        bool cut;
+        if (broad && __all(far)) {
+            d = trunc;
+            cut = true;
+        } else {
+            d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
+            cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
+            if (cut) d = trunc;
+        }
         d -= offs;  // IneqConst: dist - margin (src/planning.jl:66)
         dmin = fmin(dmin, d);
         if (dists) st_soa(dists, sp.out, ldd, off, d);
@@ -162,9 +183,16 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
                                           const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                           const CollArgs& a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                           T* __restrict__ dists, int64_t ldd, T* __restrict__ grads, int64_t ldg,
-                                          T* __restrict__ min_dist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)n) return;
+                                          T* __restrict__ min_dist, const Tiling& tl) {
+    const uint32_t b = blockIdx.x;
+    if ((uint64_t)b * blockDim.x + threadIdx.x >= (uint64_t)n) return;
+    // tiled SoA (kin_coll_batch_tiled): this workgroup's tile moves the array bases (wave-uniform)
+    const uint32_t t = b / tl.tile_blocks;
+    q += (int64_t)t * tl.tsq;
+    if (dists) dists += (int64_t)t * tl.tsp;
+    if (grads) grads += (int64_t)t * tl.tsj;
+    if (min_dist) min_dist += (int64_t)t * tl.tsm;
+    const uint32_t i = (b - t * tl.tile_blocks) * blockDim.x + threadIdx.x;
     const uint32_t off = i * (uint32_t)sizeof(T);
     const bool base = (P.flags & PF_BASE) != 0;
     T bx = T(0), by = T(0), bth = T(0);
@@ -184,6 +212,8 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     else set_identity(f);
     const T trunc = (T)a.truncation;
     const T offs = (T)a.offset;
+    const bool broad = isfinite(a.truncation);  // uniform
+    const T bnd[6] = {(T)a.bc[0], (T)a.bc[1], (T)a.bc[2], (T)a.bh[0], (T)a.bh[1], (T)a.bh[2]};
     T dmin = T(INFINITY);
     T ro[MAXA][3], rz[MAXA][3];
 #pragma unroll
@@ -192,7 +222,8 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
         rz[s][0] = rz[s][1] = rz[s][2] = T(0);
     }
     const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
-    coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs, ro,
+    coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs,
+                                broad, bnd, ro,
                                 rz, bx, by, off,
                           dists, ldd, grads, ldg, dmin);
 #pragma unroll
@@ -205,7 +236,7 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
             ro[s][2] = fma(rz[s][0], o1, -(rz[s][1] * o0));
         }
         coll_spheres<T, MAXA, GRAD>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
-                                    offs, ro, rz, bx, by, off,
+                                    offs, broad, bnd, ro, rz, bx, by, off,
                               dists, ldd, grads, ldg, dmin);
     }
     if (min_dist) {

@@ -66,7 +66,7 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
-    Tiling tl{tiled ? (uint32_t)(ta.tile / g.block) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj};
+    Tiling tl{tiled ? (uint32_t)(ta.tile / g.block) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, 0};
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         const int64_t c = std::min(chunk, n - s0);
         const dim3 grid(grid_of(c, g.block)), block(g.block);

@@ -163,6 +163,7 @@ struct kin_model {
 struct kin_sdf {
     int32_t n_boxes = 0;
     int32_t n_aabb = 0;     // the first n_aabb boxes are axis-aligned (KAabb table after the KBox array)
+    double bc[3] = {0, 0, 0}, bh[3] = {0, 0, 0};  // world-aligned box enclosing every box (broad phase, coll_body)
     void* d_f32 = nullptr;
     void* d_f64 = nullptr;
     ~kin_sdf() {
@@ -1113,6 +1114,28 @@ int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* w
             af[o].pad[0] = af[o].pad[1] = 0;
         }
     }
+    {  // enclosing world-aligned box of all box corners
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        std::vector<std::array<double, 3>> corners;
+        for (int32_t k = 0; k < n_boxes; ++k) {
+            const double* P = poses16 + 16 * k;  // column-major 4x4
+            for (int c = 0; c < 8; ++c) {
+                const double l[3] = {(c & 1 ? 0.5 : -0.5) * widths3[3 * k], (c & 2 ? 0.5 : -0.5) * widths3[3 * k + 1],
+                                     (c & 4 ? 0.5 : -0.5) * widths3[3 * k + 2]};
+                std::array<double, 3> w;
+                for (int i = 0; i < 3; ++i) {
+                    w[i] = P[12 + i] + P[i] * l[0] + P[4 + i] * l[1] + P[8 + i] * l[2];
+                    lo[i] = std::min(lo[i], w[i]);
+                    hi[i] = std::max(hi[i], w[i]);
+                }
+                corners.push_back(w);
+            }
+        }
+        for (int i = 0; i < 3; ++i) {
+            sd->bc[i] = 0.5 * (lo[i] + hi[i]);
+            sd->bh[i] = 0.5 * (hi[i] - lo[i]) * (1.0 + 1e-12) + 1e-12;
+        }
+    }
     hipError_t e = upload_boxes(&sd->d_f32, bf, af);
     if (e == hipSuccess) e = upload_boxes(&sd->d_f64, bd, ad);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("kin_sdf_create_boxes: ") + hipGetErrorString(e));
@@ -1201,7 +1224,7 @@ int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** 
 namespace {
 // k_coll over every chain program of a collision plan; min_dist accumulates after the first
 int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q, int64_t ldq, int64_t n, void* dists,
-                int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream) {
+                int64_t ldd, void* grads, int64_t ldg, void* min_dist, const TileArgs& ta, void* stream) {
     const size_t np = p->parts.empty() ? 1 : p->parts.size();
     for (size_t k = 0; k < np; ++k) {
         const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
@@ -1210,13 +1233,39 @@ int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q
         if (s->dtype == KIN_F32)
             e = launch_coll<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
                                    (const KBox<float>*)sdf->d_f32, s->geom, a, (const float*)q, ldq, n, (float*)dists,
-                                   ldd, (float*)grads, ldg, (float*)min_dist, jit_fns(s->jit), (hipStream_t)stream);
+                                   ldd, (float*)grads, ldg, (float*)min_dist, ta, jit_fns(s->jit),
+                                   (hipStream_t)stream);
         else
             e = launch_coll<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
                                     (const KBox<double>*)sdf->d_f64, s->geom, a, (const double*)q, ldq, n,
-                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, jit_fns(s->jit),
+                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, ta, jit_fns(s->jit),
                                     (hipStream_t)stream);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
+    }
+    return KIN_OK;
+}
+
+CollArgs coll_args(const kin_sdf* sdf, double truncation, double offset) {
+    return CollArgs{truncation, offset, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
+                    {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};
+}
+
+// shared checks of the collision entry points; ta.tile >= n is the plain layout
+int coll_check(const kin_plan* p, const kin_sdf* sdf, const void* q, int64_t ldq, int64_t tsq, int64_t n,
+               const void* out1, int64_t ld1, int64_t ts1, int rows1, const void* out2, int64_t ld2, int64_t ts2,
+               int rows2, const TileArgs& ta, const char* fn) {
+    auto bad = [&](const char* what) { return set_error(KIN_E_INVALID, std::string(fn) + ": " + what); };
+    if (!p || !sdf) return bad("null plan / sdf");
+    if (!p->is_coll) return bad("plan was not made by kin_coll_plan_create");
+    if (n < 0) return bad("n < 0");
+    if (n == 0) return KIN_OK;
+    const int64_t span = std::min(ta.tile, n);
+    if ((p->nqcols > 0 && (!q || ldq < span)) || (out1 && ld1 < span) || (out2 && ld2 < span))
+        return bad("bad pointer / stride");
+    if (ta.tile < n) {
+        if (ta.tile < 256 || ta.tile % 256 || ta.tile > (int64_t(1) << 26)) return bad("tile must be a multiple of 256 <= 2^26");
+        if ((p->nqcols > 0 && tsq < p->nqcols * ldq) || (out1 && ts1 < rows1 * ld1) || (out2 && ts2 < rows2 * ld2))
+            return bad("tile strides overlap");
     }
     return KIN_OK;
 }
@@ -1224,28 +1273,44 @@ int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q
 
 int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq, int64_t n,
                    void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream) {
-    if (!p || !sdf) return set_error(KIN_E_INVALID, "kin_coll_batch: null plan / sdf");
-    if (!p->is_coll) return set_error(KIN_E_INVALID, "kin_coll_batch: plan was not made by kin_coll_plan_create");
-    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
-    if (n == 0) return KIN_OK;
-    if ((p->nqcols > 0 && (!q || ldq < n)) || (dists && ldd < n) || (grads && ldg < n))
-        return set_error(KIN_E_INVALID, "kin_coll_batch: bad pointer / stride");
-    CollArgs a{truncation, 0.0, sdf->n_boxes, sdf->n_aabb, 0};
-    return coll_launch(p, sdf, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, stream);
+    const TileArgs ta = plain_soa(n);
+    const int rc = coll_check(p, sdf, q, ldq, 0, n, dists, ldd, 0, 0, grads, ldg, 0, 0, ta, "kin_coll_batch");
+    if (rc != KIN_OK || n == 0) return rc;
+    return coll_launch(p, sdf, coll_args(sdf, truncation, 0.0), q, ldq, n, dists, ldd, grads, ldg, min_dist, ta,
+                       stream);
+}
+
+int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double truncation, int64_t tile, const void* q,
+                         int64_t ldq, int64_t tsq, int64_t n, void* dists, int64_t ldd, int64_t tsd, void* grads,
+                         int64_t ldg, int64_t tsg, void* min_dist, int64_t tsm, void* stream) {
+    const TileArgs ta{tile, tsq, tsd, tsg, tsm};
+    const int ndof = p ? p->nqcols : 0;
+    int rc = coll_check(p, sdf, q, ldq, tsq, n, dists, ldd, tsd, p ? p->n_sph : 0, grads, ldg, tsg,
+                        p ? p->n_sph * ndof : 0, ta, "kin_coll_batch_tiled");
+    if (rc == KIN_OK && min_dist && tile < n && tsm < tile) rc = set_error(KIN_E_INVALID, "kin_coll_batch_tiled: tsm < tile");
+    if (rc != KIN_OK || n == 0) return rc;
+    return coll_launch(p, sdf, coll_args(sdf, truncation, 0.0), q, ldq, n, dists, ldd, grads, ldg, min_dist, ta,
+                       stream);
 }
 
 int kin_ineq_const_batch(const kin_plan* p, const kin_sdf* sdf, double margin, const void* q, int64_t ldq, int64_t n,
                          void* vals, int64_t ldv, void* jac, int64_t ldj, void* stream) {
-    if (!p || !sdf) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: null plan / sdf");
-    if (!p->is_coll) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: plan was not made by kin_coll_plan_create");
+    return kin_ineq_const_batch_tiled(p, sdf, margin, n > 0 ? n : 1, q, ldq, 0, n, vals, ldv, 0, jac, ldj, 0, stream);
+}
+
+int kin_ineq_const_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double margin, int64_t tile, const void* q,
+                               int64_t ldq, int64_t tsq, int64_t n, void* vals, int64_t ldv, int64_t tsv, void* jac,
+                               int64_t ldj, int64_t tsj, void* stream) {
     if (!std::isfinite(margin)) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: margin must be finite");
-    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
-    if (n == 0) return KIN_OK;
-    if ((p->nqcols > 0 && (!q || ldq < n)) || !vals || ldv < n || (jac && ldj < n))
-        return set_error(KIN_E_INVALID, "kin_ineq_const_batch: bad pointer / stride");
+    if (!vals) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: null vals");
+    const TileArgs ta = tile >= n ? plain_soa(n) : TileArgs{tile, tsq, tsv, tsj, 0};
+    const int ndof = p ? p->nqcols : 0;
+    const int rc = coll_check(p, sdf, q, ldq, tsq, n, vals, ldv, tsv, p ? p->n_sph : 0, jac, ldj, tsj,
+                              p ? p->n_sph * ndof : 0, ta, "kin_ineq_const_batch");
+    if (rc != KIN_OK || n == 0) return rc;
     // src/planning.jl:56, :66: truncation_dist = margin + 0.05; val = dist - margin
-    CollArgs a{margin + 0.05, margin, sdf->n_boxes, sdf->n_aabb, 0};
-    return coll_launch(p, sdf, a, q, ldq, n, vals, ldv, jac, ldj, nullptr, stream);
+    return coll_launch(p, sdf, coll_args(sdf, margin + 0.05, margin), q, ldq, n, vals, ldv, jac, ldj, nullptr, ta,
+                       stream);
 }
 
 int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, const void* q, int64_t ldq, int64_t n,

@@ -19,9 +19,10 @@ struct LaunchGeom {
 // tile >= n is the plain SoA of kin_plan_run (one tile, ts unused).
 struct TileArgs {
     int64_t tile;
-    int64_t tsq, tsp, tsj;  // tile strides (elements) of q, poses, jac
+    int64_t tsq, tsp, tsj;  // tile strides (elements) of q, poses / dists, jac / grads
+    int64_t tsm = 0;        // min_dist (k_coll)
 };
-inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0}; }
+inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0, 0}; }
 
 // Plan-specialised kernels of one plan (kinhip_jit.cpp); a null entry means
 // the generic kernel runs.
@@ -60,7 +61,8 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                        const LaunchGeom& g, const CollArgs& a, const T* q, int64_t ldq, int64_t n, T* dists,
-                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st);
+                       int64_t ldd, T* grads, int64_t ldg, T* min_dist, const TileArgs& ta, const JitFns* jf,
+                       hipStream_t st);
 
 template <typename T>
 hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,

@@ -98,7 +98,8 @@ struct KAabb {
 // kernel-side tiling: workgroup b works on tile b / tile_blocks (0xffffffff: plain SoA)
 struct Tiling {
     uint32_t tile_blocks;
-    int64_t tsq, tsp, tsj;
+    int64_t tsq, tsp, tsj;  // k_fk: q, poses, jac; k_coll: q, dists, grads
+    int64_t tsm;            // k_coll: min_dist
 };
 
 struct CollArgs {
@@ -107,6 +108,8 @@ struct CollArgs {
     int32_t n_boxes;  // KBox array (sorted: the first n_aabb are axis-aligned)
     int32_t n_aabb;   // KAabb array placed right after the KBox array
     int32_t accumulate;  // min_dist = min(min_dist, this launch's minimum) (multi-chain plans)
+    int32_t pad;
+    double bc[3], bh[3];  // world-aligned box enclosing the union: centre, half extents (broad phase)
 };
 
 template <typename T>

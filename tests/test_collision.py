@@ -299,3 +299,66 @@ def test_gpu_collision_specialized_equals_generic(dtype, with_base):
         b = sscc.plan(joints, dtype=dtype).specialize().run(sdf, Q2, grads=True, min_dist=True)
         for x, y in zip(a, b):
             assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("spec", [False, True])
+def test_gpu_collision_broad_phase_exact(dtype, spec):
+    """Finite truncation enables the broad phase (spheres provably beyond truncation + the union's
+    bounding sphere skip the boxes wave-wide).  Its results must equal the exact evaluation clamped
+    afterwards: distances min(d, trunc), gradients zero where d > trunc -- for a scene where every
+    wave skips (boxes far away), one where none can, and the fridge (mixed)."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    g = torch.Generator().manual_seed(8)
+    N = 4096
+    Q = (torch.rand((8, N), generator=g, dtype=torch.float64) * 3 - 1.5).to(dtype).to(dev)
+    for base, trunc in (((6.0, 0.0, 0.0), 0.05), ((1.2, 0.0, 0.0), 0.08), ((0.3, 0.0, 0.0), 0.02)):
+        poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=base)
+        sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+        plan = sscc.plan(arm, dtype=dtype)
+        if spec:
+            plan.specialize()
+        D0, G0, _ = plan.run(sdf, Q, grads=True)                   # exact (no truncation)
+        D1, G1, M1 = plan.run(sdf, Q, grads=True, min_dist=True, truncation=trunc)
+        far = D0 > trunc
+        assert torch.equal(D1, torch.where(far, torch.full_like(D0, trunc), D0))
+        assert torch.equal(G1, torch.where(far.unsqueeze(1), torch.zeros_like(G0), G0))
+        assert torch.equal(M1, D1.min(0).values)
+        if base[0] > 5:
+            assert bool(far.all())  # every sphere skipped the boxes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("spec", [False, True])
+def test_gpu_collision_tiled_layout(dtype, spec):
+    """kin_coll_batch_tiled / kin_ineq_const_batch_tiled == the plain layout, bit for bit (partial last
+    tile, one tile, multi-chain plan, min distance accumulated across chains)."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=(1.2, 0.0, 0.0))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    sscc.add_coll_sphere(m.find_link("head_pan_link"), (0.05, 0.0, 0.1), 0.12)
+    joints = arm + [m.find_joint("head_pan_joint"), m.find_joint("head_tilt_joint")]
+    plan = sscc.plan(joints, dtype=dtype)
+    if spec:
+        plan.specialize()
+    g = torch.Generator().manual_seed(12)
+    for N, tile in ((3000, 256), (5000, 1024), (600, 1024)):
+        Q = (torch.rand((10, N), generator=g, dtype=torch.float64) * 3 - 1.5).to(dtype).to(dev)
+        D0, G0, M0 = plan.run(sdf, Q, grads=True, min_dist=True, truncation=0.2)
+        Dt, Gt, Mt = plan.run_tiled(sdf, kinhip.tiled(Q, tile), N, grads=True, min_dist=True, truncation=0.2)
+        assert torch.equal(kinhip.untiled(Dt, N), D0) and torch.equal(kinhip.untiled(Gt, N), G0)
+        assert torch.equal(kinhip.untiled(Mt, N), M0)
+        ic = kinhip.IneqConst(sscc, joints, sdf, 1, 0.03, dtype=dtype)
+        if spec:
+            ic.plan.specialize()
+        V0, J0 = ic.eval_batch(Q)
+        Vt, Jt = ic.eval_batch_tiled(kinhip.tiled(Q, tile), N)
+        assert torch.equal(kinhip.untiled(Vt, N), V0) and torch.equal(kinhip.untiled(Jt, N), J0)
