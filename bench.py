@@ -235,8 +235,9 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
         nx = Qx.shape[1]
         out[name] = {"value": nx * ctx.world * steps / wall,
                      "unit": "waypoints/s (values + gradients)" if name.startswith("ineq") else "FK+SDF samples/s",
-                     "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
-                     "achieved_GBs": nbytes * nx / (dev_s / steps) / 1e9}
+                     "algorithmic_bytes_per_sample": 36 if name.startswith("min_dist") else nbytes,
+                     "avg_launch_us": dev_s / steps * 1e6,
+                     "achieved_GBs": (36 if name.startswith("min_dist") else nbytes) * nx / (dev_s / steps) / 1e9}
         if name.startswith("ineq"):
             out[name]["margin"] = 0.03
         if name.endswith("tiled"):
