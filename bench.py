@@ -94,12 +94,11 @@ def _time_tiled(plan, Qt, n, poses, jac, steps, warmup, ctx, stream):
     return D.max_over_ranks(ctx, [wall, dev_s])
 
 
-def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5, spec=1):
+def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5, spec=1, dt=torch.float32):
     """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
     <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
     Multi-GPU: the solutions (8 angles) and iteration counts are all-gathered to every rank over
     RCCL afterwards -- timed separately, not part of the solve rate."""
-    dt = torch.float32
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     if spec:
         _specialize(plan, kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
@@ -125,7 +124,8 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5, spec=1):
     wall = D.max_over_ranks(ctx, [time.perf_counter() - t0])[0]
     succ = (it < 64).float().mean()
     out = {"value": n * ctx.world * reps / wall, "unit": "IK solves/s", "targets_per_gpu": n,
-           "success_rate": float(succ), "ms_per_batch": wall / reps * 1e3, "dtype": "f32",
+           "success_rate": float(succ), "ms_per_batch": wall / reps * 1e3,
+           "dtype": "f32" if dt == torch.float32 else "f64",
            "params": "DLS lambda=1e-2, max_step=0.5, 64 iters incl. 3 seeded restarts, q0=0",
            "kernels": "specialised" if spec else "generic"}
     if ctx.world > 1:
@@ -503,6 +503,7 @@ def main():
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": lay64}
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec)
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
+        out["config4_ik_dls_f64"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, dt=torch.float64)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec)
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
         if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)
