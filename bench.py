@@ -458,6 +458,14 @@ def main():
         out["config"]["layout"] = f"plain SoA (kin_plan_run), rows padded to ld = N + {args.row_pad}"
     if args.extras:
         out["roofline"]["measured_copy_GBs"] = _copy_bw(dev)
+    if args.extras and headline_spec:
+        # the same workload through the most literal form of the API: generic kernel (no run-time
+        # compilation), plain column-major rows (padded ld) -- kin_plan_run as a Julia caller would
+        # use it first; its kernel (k_fk<float, 8>) is profiled apart from the headline's
+        wg, dg = timed_leg(torch.float32, True, [gl], "generic_soa")
+        out["fk_jac_f32_generic_plain_soa"] = {"value": N * ws * args.steps / wg, "unit": "evals/s",
+                                               "avg_launch_us": dg / args.steps * 1e6,
+                                               "achieved_GBs": bytes_per_eval * N / (dg / args.steps) / 1e9}
     if args.sweep:
         # the same workload in the other layouts: plain SoA (padded and unpadded rows), other tiles
         lay = {}
