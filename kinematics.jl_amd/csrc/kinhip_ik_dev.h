@@ -284,7 +284,8 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         for (int s = 0; s < MAXA; ++s) w[s] = T(1);
         T dq[MAXA], db[3] = {T(0), T(0), T(0)};
         T mx = T(0);
-        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {  // unrolled: pass 0 has w == 1 as a constant
             // A = J W J^T + lambda^2 I  (lower triangle)
             T A[ROWS][ROWS];
 #pragma unroll
