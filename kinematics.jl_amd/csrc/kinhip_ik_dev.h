@@ -48,6 +48,20 @@ __device__ __forceinline__ void jcol(const KStep<T>& st, const T (&o)[3], const 
     }
 }
 
+// jcol with the linear part z x (p - o) already formed (ik_body computes it once per
+// iteration into the record's origin slot: o := z x (p - o))
+template <typename T, int ROWS>
+__device__ __forceinline__ void jcol_pre(const KStep<T>& st, const T (&lin)[3], const T (&z)[3], T (&J)[ROWS]) {
+    const T m = (st.flags & SF_REC) ? T(1) : T(0);
+    if (st.jkind == MOT_PRISM) {
+        J[0] = m * z[0]; J[1] = m * z[1]; J[2] = m * z[2];
+        if constexpr (ROWS == 6) { J[3] = T(0); J[4] = T(0); J[5] = T(0); }
+    } else {
+        J[0] = m * lin[0]; J[1] = m * lin[1]; J[2] = m * lin[2];
+        if constexpr (ROWS == 6) { J[3] = m * z[0]; J[4] = m * z[1]; J[5] = m * z[2]; }
+    }
+}
+
 // world rotation vector w with exp([w]) R = Rt  (log of Rt R^T)
 template <typename T>
 __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (&w)[3]) {
@@ -279,6 +293,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         // pass 0: every joint; pass 1 (lanes that need it): joints sitting on a
         // limit that the step pushes further out get weight 0 and the system is
         // re-solved (same rule as the oracle's or_ik_dls_batch)
+        // linear Jacobian rows z x (p - o) once per iteration (both passes and dq reuse them)
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) {
+            const T dx = Lf.t[0] - ro[s][0], dy = Lf.t[1] - ro[s][1], dz = Lf.t[2] - ro[s][2];
+            ro[s][0] = fma(rz[s][1], dz, -(rz[s][2] * dy));
+            ro[s][1] = fma(rz[s][2], dx, -(rz[s][0] * dz));
+            ro[s][2] = fma(rz[s][0], dy, -(rz[s][1] * dx));
+        }
         T w[MAXA];
 #pragma unroll
         for (int s = 0; s < MAXA; ++s) w[s] = T(1);
@@ -295,7 +317,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
+                jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) J[r] *= w[s];
 #pragma unroll
@@ -360,7 +382,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
-                jcol<T, ROWS>(S[s], ro[s], rz[s], Lf, J);
+                jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
                 T v = T(0);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
