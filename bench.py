@@ -457,7 +457,7 @@ def main():
     else:
         out["config"]["layout"] = f"plain SoA (kin_plan_run), rows padded to ld = N + {args.row_pad}"
     if args.extras:
-        out["roofline"]["measured_copy_GBs"] = _copy_bw(dev)
+        out["roofline"]["torch_copy_GBs"] = _copy_bw(dev)  # context: torch device-to-device copy rate
     if args.extras and headline_spec:
         # the same workload through the most literal form of the API: generic kernel (no run-time
         # compilation), plain column-major rows (padded ld) -- kin_plan_run as a Julia caller would
