@@ -53,6 +53,9 @@ def test_ground_truth_json_on_gpu(dev, with_base):
     angles = list(gt["angle_vector"]) + ([0.3, 0.3, 0.3] if with_base else [])
     Q = torch.tensor(angles, dtype=torch.float64, device=dev).reshape(-1, 1).repeat(1, 3).contiguous()
     poses = kinhip.get_transform_batch(m, links, joints, Q).cpu().numpy()
+    # the same request through a plan-specialised kernel (constants of the PR2 fragment folded)
+    ps = m.plan(joints, out_links=links, dtype=torch.float64).specialize(kinhip.KIN_SPEC_FK).run(Q)[0]
+    np.testing.assert_array_equal(ps.cpu().numpy(), poses)
     th = 0.3
     Rz = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
     for rep in range(2):
@@ -88,6 +91,12 @@ def test_golden_fetch_fixture(dev, dtype):
     pose, jac = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True)
     np.testing.assert_allclose(jac.double().cpu().numpy(), g["jac_geo"], atol=tol)
     np.testing.assert_allclose(pose.double().cpu().numpy(), g["poses"][gl.id - 1], atol=tol)
+    # the bench's path: specialised plan, tiled layout, against the same golden vectors
+    sp = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype).specialize(kinhip.KIN_SPEC_FK)
+    Pt, Jt = sp.run_tiled(kinhip.tiled(Q, 256), Q.shape[1])
+    np.testing.assert_allclose(kinhip.untiled(Jt, Q.shape[1]).double().cpu().numpy(), g["jac_geo"], atol=tol)
+    np.testing.assert_allclose(kinhip.untiled(Pt, Q.shape[1])[0].double().cpu().numpy(), g["poses"][gl.id - 1],
+                               atol=tol)
     _, jr = kinhip.get_jacobian_batch(m, gl, arm, Q, with_rot=True, rpy_jac=True)
     jr = jr.double().cpu().numpy()
     ok = np.abs(np.cos(np.arcsin(np.clip(-g["poses"][gl.id - 1][2], -1, 1)))) > 1e-2  # away from pitch = +-pi/2
