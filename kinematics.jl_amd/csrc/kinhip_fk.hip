@@ -79,8 +79,8 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
             int64_t cc = c;
             void* args[] = {(void*)&qc, (void*)&ldq, (void*)&cc, (void*)&pc, (void*)&ldp, (void*)&jc, (void*)&ldj,
                             (void*)&tl};
-            const hipError_t e = hipModuleLaunchKernel(jit, grid.x, 1, 1, block.x, 1, 1, (unsigned)g.lds, st, args,
-                                                       nullptr);
+            // (specialised kernels keep branch frames in registers: no dynamic LDS)
+            const hipError_t e = hipModuleLaunchKernel(jit, grid.x, 1, 1, block.x, 1, 1, 0, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }

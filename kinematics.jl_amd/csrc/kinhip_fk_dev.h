@@ -19,6 +19,16 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
                                         const T* __restrict__ q, int64_t ldq, int64_t n, T* __restrict__ poses,
                                         int64_t ldp, T* __restrict__ jac, int64_t ldj, const Tiling& tl) {
     const int B = blockDim.x, tid = threadIdx.x;
+#ifdef KINHIP_JIT
+    // specialised kernels: every slot index is a constant, so branch frames live in registers
+    // (the array is scalar-replaced) instead of per-lane LDS slots
+    Fr<T> rslot[kMaxSlots];
+#define KIN_SLOT_STORE(sl, fr) rslot[sl] = (fr)
+#define KIN_SLOT_LOAD(sl, fr) (fr) = rslot[sl]
+#else
+#define KIN_SLOT_STORE(sl, fr) slot_store(slots, (sl), B, tid, (fr))
+#define KIN_SLOT_LOAD(sl, fr) slot_load(slots, (sl), B, tid, (fr))
+#endif
     const uint32_t b = config_block();
     if ((uint64_t)b * (uint32_t)B + tid >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
     // tiled SoA: this workgroup's tile (wave-uniform) moves the array bases; lanes keep a 32-bit offset
@@ -63,7 +73,7 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
             link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
             store_pose(sk, poses, st.out, ldp, L);
         }
-        if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
+        if (st.save >= 0) KIN_SLOT_STORE(st.save, f);
     }
 
     if ((P.flags & PF_JAC) || P.spine_out >= 0) {
@@ -117,11 +127,14 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
     }
 
     // phase B: the remaining links (uniform loop, LDS slots at branch points)
+#ifdef KINHIP_JIT
+#pragma unroll
+#endif
     for (int s = P.nA; s < P.nS; ++s) {
         const KStep<T>& st = S[s];
         const int32_t ld = st.load;
         if (ld == LOAD_ROOT) f = root;
-        else if (ld >= 0) slot_load(slots, ld, B, tid, f);
+        else if (ld >= 0) KIN_SLOT_LOAD(ld, f);
         mul_rigid(f, st.F);
         if (st.kind != MOT_NONE) motion(f, st.kind, st.flags, st.scale, ld_soa(q, st.qcol, ldq, off));
         if (st.out >= 0) {
@@ -129,9 +142,11 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
             link_frame(L, f, (st.flags & SF_HAS_X) != 0, st.X);
             store_pose(sk, poses, st.out, ldp, L);
         }
-        if (st.save >= 0) slot_store(slots, st.save, B, tid, f);
+        if (st.save >= 0) KIN_SLOT_STORE(st.save, f);
     }
 }
 
+#undef KIN_SLOT_STORE
+#undef KIN_SLOT_LOAD
 }  // namespace
 }  // namespace kinhip
