@@ -85,8 +85,10 @@ class SweptSphereCollisionChecker:
         self.sphere_radii.append(float(radius))
         return sl
 
-    def plan(self, joints, dtype=torch.float32) -> "CollisionPlan":
-        return CollisionPlan(self, joints, dtype)
+    def plan(self, joints, dtype=torch.float32, specialize=False) -> "CollisionPlan":
+        """kin_coll_plan_create; `specialize=True` also compiles it (kin_plan_specialize)."""
+        p = CollisionPlan(self, joints, dtype)
+        return p.specialize() if specialize else p
 
 
 class CollisionPlan:

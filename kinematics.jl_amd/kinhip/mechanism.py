@@ -212,9 +212,14 @@ class Mechanism:
     # -- batched hot path -------------------------------------------------------
     def plan(self, q_joints: Sequence[Joint], out_links: Sequence[Link] = (), jac_link: Optional[Link] = None,
              jac_joints: Optional[Sequence[Joint]] = None, with_rot: bool = True, rpy_jac: bool = False,
-             zero_fill: bool = True, dtype=torch.float32) -> "Plan":
+             zero_fill: bool = True, dtype=torch.float32, specialize=False) -> "Plan":
+        """A staged evaluation program (kin_plan_create).  `specialize`: True (every kernel kind that
+        applies) or a KIN_SPEC_* mask compiles it into constant-folded kernels (kin_plan_specialize)."""
         self._sync_angles()
-        return Plan(self, q_joints, out_links, jac_link, jac_joints, with_rot, rpy_jac, zero_fill, dtype)
+        p = Plan(self, q_joints, out_links, jac_link, jac_joints, with_rot, rpy_jac, zero_fill, dtype)
+        if specialize:
+            p.specialize(0 if specialize is True else int(specialize))
+        return p
 
 
 class Plan:
