@@ -233,7 +233,21 @@ __device__ __forceinline__ void mul_rigid_regs(Fr<T>& out, const Fr<T>& f, const
 
 // joint motion in the canonical frame (axis = local z), branch-free in the
 // joint kind: revolute -> (c, s, 0), prismatic -> (1, 0, scale*q), none -> (1, 0, 0)
-template <typename T>
+// Trig for the joint angle.  FT (fast trig, fp32 IK only): the hardware v_sin_f32 / v_cos_f32
+// (max abs error 3.6e-7 over [-3.5, 3.5], tools/sin_probe.hip) instead of the ~20-instruction
+// reduction + polynomial -- inside an iterative solver checked against a 1e-3 tolerance.
+template <bool FT, typename T>
+__device__ __forceinline__ void joint_sincos(T th, T* s, T* c) {
+    if constexpr (FT && sizeof(T) == 4) {
+        const float r = th * 0.15915494309189535f;  // the hardware ops take revolutions
+        *s = __builtin_amdgcn_sinf(r);
+        *c = __builtin_amdgcn_cosf(r);
+    } else {
+        sincos_t(th, s, c);
+    }
+}
+
+template <typename T, bool FT = false>
 __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T scale, T qv) {
     if (__builtin_constant_p(kind) && __builtin_constant_p(flags)) {  // specialised plan: kind known
         if (kind == MOT_REV) {
@@ -244,7 +258,7 @@ __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T 
                 th = T(2) * atan2_t(scale * sh, ch);
             }
             T s, c;
-            sincos_t(th, &s, &c);
+            joint_sincos<FT>(th, &s, &c);
 #pragma unroll
             for (int i = 0; i < 3; ++i) {
                 const T a = f.r[3 * i], b = f.r[3 * i + 1];
@@ -268,7 +282,7 @@ __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T 
         th = T(2) * atan2_t(scale * sh, ch);
     }
     T s, c;
-    sincos_t(th, &s, &c);
+    joint_sincos<FT>(th, &s, &c);
     const T d = (kind == MOT_PRISM) ? scale * qv : T(0);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -347,13 +361,13 @@ __device__ __forceinline__ void slot_load(const T* slots, int slot, int B, int t
 
 // One phase-A step: C <- C F; record (o, z); motion.  Straight-line: padded
 // steps are identities with scale 0, so records and motion need no branch.
-template <typename T>
+template <typename T, bool FT = false>
 __device__ __forceinline__ void step_a(Fr<T>& f, const KStep<T>& st, T qv, T (&o)[3], T (&z)[3]) {
     mul_rigid(f, st.F);
     o[0] = f.t[0]; o[1] = f.t[1]; o[2] = f.t[2];  // _get_joint_axis, src/algorithm.jl:42-54
     const T sc = st.scale;
     z[0] = f.r[2] * sc; z[1] = f.r[5] * sc; z[2] = f.r[8] * sc;
-    motion(f, st.kind, st.flags, sc, qv);
+    motion<T, FT>(f, st.kind, st.flags, sc, qv);
 }
 
 // One get_jacobian! column (src/algorithm.jl:65-81): revolute -> [z x (p - o); z or

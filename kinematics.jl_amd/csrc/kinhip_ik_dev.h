@@ -27,7 +27,7 @@ __device__ __forceinline__ void chain_records(const KProg<T>& P, const KStep<T>*
                                               T (&ro)[MAXA][3], T (&rz)[MAXA][3]) {
     Fr<T> f = root;
 #pragma unroll
-    for (int s = 0; s < MAXA; ++s) step_a(f, S[s], qs[s], ro[s], rz[s]);
+    for (int s = 0; s < MAXA; ++s) step_a<T, true>(f, S[s], qs[s], ro[s], rz[s]);  // fast trig (fp32)
     link_frame(L, f, P.last_has_x != 0, P.Xlast);
 }
 
