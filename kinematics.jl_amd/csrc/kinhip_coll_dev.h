@@ -4,6 +4,10 @@
 #pragma once
 #include "kinhip_device.h"
 
+#ifndef KINHIP_COLL_FAST_TRIG
+#define KINHIP_COLL_FAST_TRIG 1  // fp32: hardware sin/cos for the chain (joint_sincos, ~4e-7 abs error)
+#endif
+
 namespace kinhip {
 namespace {
 
@@ -228,7 +232,7 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
                           dists, ldd, grads, ldg, dmin);
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
-        step_a(f, S[s], qa[s], ro[s], rz[s]);
+        step_a<T, KINHIP_COLL_FAST_TRIG != 0>(f, S[s], qa[s], ro[s], rz[s]);  // fp32 fast trig: see top
         if (GRAD) {  // m_s = z_s x o_s (held in ro)
             const T o0 = ro[s][0], o1 = ro[s][1], o2 = ro[s][2];
             ro[s][0] = fma(rz[s][1], o2, -(rz[s][2] * o1));
