@@ -6,6 +6,7 @@
 // Build: hipcc -O3 --offload-arch=gfx950 tools/tile_probe.hip -o gpurun_out/tile_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e)); return 1; } } while (0)
 
@@ -52,8 +53,8 @@ __global__ void p_fill(float4* __restrict__ out, long m4) {
     if (i < m4) out[i] = float4{1, 2, 3, 4};
 }
 
-int main() {
-    const int R = 60;
+int main(int argc, char** argv) {
+    const int R = argc > 1 ? atoi(argv[1]) : 60;  // output rows per configuration
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
