@@ -561,3 +561,53 @@ def test_specialize_errors(dev):
         p.specialize(kinhip.KIN_SPEC_COLL)
     assert p.specialized == 0
     assert p.specialize().specialized == kinhip.KIN_SPEC_FK
+
+
+def test_launch_chunk_boundary(dev, fetch_tree):
+    """Batches beyond one launch chunk (2^27 configurations: lane byte offsets stay 32-bit): the
+    configurations on both sides of the chunk seam and at the tail are correct in the plain layout
+    (generic kernel) and the tiled layout (specialised kernel).  FK only, fp32, ~11 GB per layout."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    N = (1 << 27) + 3000
+    lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
+    Q = kinhip.uniform_configs(lo, hi, N, dtype=torch.float32, device=dev)
+    idx = torch.cat([torch.arange(0, 64), torch.arange((1 << 27) - 300, (1 << 27) + 300),
+                     torch.arange(N - 64, N)]).to(dev)
+    om = O.OracleMech(fetch_tree)
+    ref = om.fk_batch(Q[:, idx].double().cpu().numpy(), [j.id for j in arm], [gl.id])
+    plan = m.plan(arm, out_links=[gl], dtype=torch.float32)
+    P = plan.run(Q)[0]
+    np.testing.assert_allclose(P[:, :, idx].double().cpu().numpy(), ref, atol=2e-5)
+    del P
+    tile = 8192
+    Qt = kinhip.tiled(Q, tile)
+    del Q
+    torch.cuda.empty_cache()
+    sp = m.plan(arm, out_links=[gl], dtype=torch.float32, specialize=kinhip.KIN_SPEC_FK)
+    Pt = sp.run_tiled(Qt, N)[0]
+    sel = Pt[idx // tile, :, :, idx % tile]  # (len(idx), 1, 12)
+    np.testing.assert_allclose(sel.permute(1, 2, 0).double().cpu().numpy(), ref, atol=2e-5)
+
+
+def test_ik_launch_chunk_boundary(dev):
+    """IK batches beyond one IK launch chunk (2^24 targets), specialised kernel: targets on both sides
+    of the seam and at the tail converge, and their solutions reproduce the target (exact FK)."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    N = (1 << 24) + 1000
+    lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
+    Qt = kinhip.uniform_configs(lo, hi, N, seed=31, dtype=torch.float32, device=dev)
+    fk = m.plan(arm, out_links=[gl], dtype=torch.float32)
+    tgt = fk.run(Qt)[0][0].contiguous()
+    del Qt
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32, specialize=True)
+    Q, it, err = plan.ik_dls(tgt, torch.zeros((8, N), dtype=torch.float32, device=dev), max_iters=64, restarts=3)
+    idx = torch.cat([torch.arange(0, 256), torch.arange((1 << 24) - 512, (1 << 24) + 512),
+                     torch.arange(N - 256, N)]).to(dev)
+    ok = it[idx] < 64
+    assert float(ok.float().mean()) > 0.98
+    assert float((it < 64).float().mean()) > 0.99
+    P = fk.run(Q[:, idx].contiguous())[0][0]
+    dp = (P[9:12] - tgt[9:12, idx]).norm(dim=0)
+    assert float(dp[ok].max()) < 2e-3
