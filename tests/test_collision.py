@@ -362,3 +362,26 @@ def test_gpu_collision_tiled_layout(dtype, spec):
         V0, J0 = ic.eval_batch(Q)
         Vt, Jt = ic.eval_batch_tiled(kinhip.tiled(Q, tile), N)
         assert torch.equal(kinhip.untiled(Vt, N), V0) and torch.equal(kinhip.untiled(Jt, N), J0)
+
+
+@pytest.mark.gpu
+def test_gpu_collision_launch_chunk_boundary():
+    """Collision batches beyond one launch chunk (2^27 configurations), specialised kernel, fp32: the
+    minimum distance on both sides of the seam and at the tail against the oracle."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    poses, widths = O.fridge_boxes(fr_tree, door_angle=2.0, base=(1.2, 0.0, 0.0))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    N = (1 << 27) + 2000
+    Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=3,
+                               dtype=torch.float32, device=dev)
+    plan = sscc.plan(arm, dtype=torch.float32, specialize=True)
+    _, _, Mn = plan.run(sdf, Q, dists=False, min_dist=True)
+    idx = torch.cat([torch.arange(0, 100), torch.arange((1 << 27) - 200, (1 << 27) + 200),
+                     torch.arange(N - 100, N)]).to(dev)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    ids = [tree.joint_id(n) for n in ARM]
+    rd, _ = O.coll_batch(om, O.OracleUnionSDF(poses, widths), Q[:, idx].double().cpu().numpy(), ids, sph, rad)
+    np.testing.assert_allclose(Mn[idx].double().cpu().numpy(), rd.min(0), atol=2e-5)
