@@ -189,7 +189,7 @@ KINHIP_API int kin_plan_run_tiled(const kin_plan* p, int64_t tile, const void* q
  * the two compilations contract a product-sum differently.
  * KIN_E_DEVICE (message from hiprtc) leaves the plan on its generic kernels. */
 enum {
-    KIN_SPEC_FK = 1u,        /* kin_plan_run(_tiled), kin_get_*_batch, kin_pose_const_batch */
+    KIN_SPEC_FK = 1u,        /* kin_plan_run(_tiled), kin_pose_const_batch (not the one-shot kin_get_*_batch) */
     KIN_SPEC_IK = 2u,        /* kin_ik_dls_batch (with_rot 0/1, every lane count) */
     KIN_SPEC_NAKAMURA = 4u,  /* kin_point_ik_nakamura_batch */
     KIN_SPEC_COLL = 8u       /* kin_coll_batch, kin_ineq_const_batch (spheres folded; boxes stay data) */
@@ -226,7 +226,11 @@ KINHIP_API int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_
  *   target : [12][ldt] target poses (3x4 column-major)
  *   q      : [n_qcols][ldq] initial angles in, solution out (clamped to limits)
  *   iters  : [n] int32 iterations used (== max_iters => not converged) or NULL
- *   err    : [2][n] final |dp|, |rot err| (dtype) or NULL                       */
+ *   err    : [2][n] final |dp|, |rot err| (dtype) or NULL
+ * Precision: fp64 uses exact arithmetic throughout (its iterates match the CPU
+ * restatement); fp32 uses the hardware sin / cos / rsqrt / rcp / sqrt (~1e-7..4e-7
+ * error) inside the iteration -- the result is still checked against tol_pos /
+ * tol_rot by the same iteration.                                                 */
 typedef struct kin_ik_params {
     int32_t max_iters;  /* e.g. 64 */
     double lambda;      /* damping, e.g. 1e-2 */
