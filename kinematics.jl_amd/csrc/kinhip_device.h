@@ -123,6 +123,27 @@ __device__ __forceinline__ float rsqrt_fast(float x) { return __builtin_amdgcn_r
 __device__ __forceinline__ double rsqrt_fast(double x) { return 1.0 / sqrt(x); }
 __device__ __forceinline__ float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ double rcp_fast(double x) { return 1.0 / x; }
+// atan2(s, c) for s >= 0 (the IK rotation angle, in [0, pi]).  fp32: octant reduction to
+// a = min/max in [0, 1] and atan(a) = a (1 + z P(z)), z = a^2, P a degree-6 fit
+// (max abs error 1.5e-7 on [0, 1], 3.1e-7 for the angle on [0, pi], fp32; tools/atan_fit.py);
+// fp64: atan2.
+__device__ __forceinline__ float atan2_pos_fast(float s, float c) {
+    const float ac = fabsf(c);
+    const float mx = fmaxf(s, ac), mn = fminf(s, ac);
+    const float a = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    const float z = a * a;
+    float p = -0.00435495f;
+    p = fmaf(p, z, 0.02303899f);
+    p = fmaf(p, z, -0.05777276f);
+    p = fmaf(p, z, 0.0979424f);
+    p = fmaf(p, z, -0.13976611f);
+    p = fmaf(p, z, 0.19962715f);
+    p = fmaf(p, z, -0.3333166f);
+    float r = fmaf(a * z, p, a);
+    r = s > ac ? 1.57079633f - r : r;
+    return c < 0.0f ? 3.14159265f - r : r;
+}
+__device__ __forceinline__ double atan2_pos_fast(double s, double c) { return atan2(s, c); }
 
 // SoA addressing: element `row` of a [rows][ld] array for this lane.  Each
 // row gets a wave-uniform buffer descriptor (SGPRs: base = row pointer) and

@@ -10,6 +10,9 @@ namespace {
 #ifndef KINHIP_IK_NARROW
 #define KINHIP_IK_NARROW 0  // 1: narrow SoA addressing (ldn_soa) in k_ik_dls, see kinhip_device.h
 #endif
+#ifndef KINHIP_IK_FAST_ATAN
+#define KINHIP_IK_FAST_ATAN 1  // fp32: polynomial atan2 for the rotation error's angle (rot_error)
+#endif
 #if KINHIP_IK_NARROW
 #define KIN_IK_LD ldn_soa
 #define KIN_IK_ST stn_soa
@@ -76,7 +79,11 @@ __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (
     const T v2 = T(0.5) * (E[3] - E[1]);
     const T s = sqrt_fast(v0 * v0 + v1 * v1 + v2 * v2);
     const T c = T(0.5) * (E[0] + E[4] + E[8] - T(1));
+#if KINHIP_IK_FAST_ATAN
+    const T th = atan2_pos_fast(s, c);  // fp32: polynomial, 3.1e-7 abs (kinhip_device.h)
+#else
     const T th = atan2_t(s, c);
+#endif
     if (s > T(1e-7)) {
         T k;
         if constexpr (sizeof(T) == 4) k = th * rcp_fast(s);
