@@ -94,7 +94,7 @@ def _time_tiled(plan, Qt, n, poses, jac, steps, warmup, ctx, stream):
     return D.max_over_ranks(ctx, [wall, dev_s])
 
 
-def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=5, spec=1, dt=torch.float32):
+def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=20, spec=1, dt=torch.float32):
     """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
     <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
     Multi-GPU: the solutions (8 angles) and iteration counts are all-gathered to every rank over

@@ -228,8 +228,8 @@ KINHIP_API int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_
  *   iters  : [n] int32 iterations used (== max_iters => not converged) or NULL
  *   err    : [2][n] final |dp|, |rot err| (dtype) or NULL
  * Precision: fp64 uses exact arithmetic throughout (its iterates match the CPU
- * restatement); fp32 uses the hardware sin / cos / rsqrt / rcp / sqrt (~1e-7..4e-7
- * error) inside the iteration -- the result is still checked against tol_pos /
+ * restatement); fp32 uses the hardware sin / cos / rsqrt / rcp / sqrt and a
+ * polynomial atan2 (~1e-7..4e-7 error) inside the iteration -- the result is still checked against tol_pos /
  * tol_rot by the same iteration.                                                 */
 typedef struct kin_ik_params {
     int32_t max_iters;  /* e.g. 64 */
