@@ -6,6 +6,7 @@
    box collision metadata) on fetch.urdf, fridge.urdf and the PR2 fragment
  - Mechanism host mirror: tree queries and rptable facts of test/test_mechanism.jl,
    add_new_link, KeyError / MethodError behaviour, malformed trees rejected
+ - the fp32 atan2 polynomial's constants in kinhip_device.h (host evaluation)
 """
 import ctypes as C
 import os
@@ -205,3 +206,30 @@ def test_jit_selfcheck_compiles_on_host():
     msg = K.lib().kin_last_error()
     assert rc == K.KIN_OK, (msg or b"").decode()[:2000]
     assert time.perf_counter() - t0 < 120
+
+
+def test_fp32_atan2_polynomial_constants():
+    """atan2_pos_fast (kinhip_device.h, the fp32 IK's rotation-error angle): the coefficients in
+    the header, evaluated in fp32 with the device's octant reduction, stay within 4e-7 of atan2
+    over [0, pi] (the fit is tools/atan_fit.py)."""
+    src = open(os.path.join(ROOT, "kinematics.jl_amd", "csrc", "kinhip_device.h")).read()
+    body = src[src.index("float atan2_pos_fast(float s, float c)"):]
+    body = body[:body.index("\n}\n")]
+    cf = [float(x) for x in re.findall(r"p = (?:fmaf\(p, z, )?(-?[0-9.]+)f", body)]
+    assert len(cf) == 7
+    f = np.float32
+    th = np.linspace(0.0, np.pi, 400001)
+    for rad in (1.0, 0.25, 1e-3):
+        s, c = (rad * np.sin(th)).astype(f), (rad * np.cos(th)).astype(f)
+        ac = np.abs(c)
+        mx, mn = np.maximum(s, ac), np.minimum(s, ac)
+        a = np.where(mx > 0, mn / np.where(mx > 0, mx, f(1)), f(0)).astype(f)
+        z = a * a
+        p = f(cf[0])
+        for k in cf[1:]:
+            p = (p * z + f(k)).astype(f)
+        r = (a * z * p + a).astype(f)
+        r = np.where(s > ac, f(1.57079633) - r, r)
+        r = np.where(c < 0, f(3.14159265) - r, r)
+        ref = np.arctan2(s.astype(np.float64), c.astype(np.float64))
+        assert np.abs(r.astype(np.float64) - ref).max() < 4e-7
