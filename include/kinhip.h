@@ -33,6 +33,10 @@
  *  - Thread safety: models/plans are immutable after creation except through
  *    kin_model_set_angles / kin_model_add_link (not concurrent with use).
  *    Distinct streams may run plans concurrently from different host threads.
+ *  - Devices: a plan / kin_sdf belongs to the HIP device that was current when
+ *    it was created.  Every run / specialise call checks the current device
+ *    and returns KIN_E_INVALID on a mismatch (one plan per device for
+ *    multi-GPU callers); kin_get_*_batch keep one cached plan per device.
  */
 #ifndef KINHIP_H
 #define KINHIP_H
@@ -225,7 +229,8 @@ KINHIP_API int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_
  * and jac_flags without KIN_RPY_JAC; its jac link is the IK target link.
  *   target : [12][ldt] target poses (3x4 column-major)
  *   q      : [n_qcols][ldq] initial angles in, solution out (clamped to limits)
- *   iters  : [n] int32 iterations used (== max_iters => not converged) or NULL
+ *   iters  : [n] int32 or NULL: the iterations the converged attempt used (0..max_iters, so a target
+ *            converging at exactly max_iters reports max_iters), max_iters + 1 if no attempt converged
  *   err    : [2][n] final |dp|, |rot err| (dtype) or NULL
  * Precision: fp64 uses exact arithmetic throughout (its iterates match the CPU
  * restatement); fp32 uses the hardware sin / cos / rsqrt / rcp / sqrt and a
@@ -245,6 +250,9 @@ typedef struct kin_ik_params {
     int32_t lanes;      /* lanes per target running attempts side by side: 0 = auto, else 1/2/4/8.
                            Results are identical for every value (each attempt's arithmetic is the
                            sequential schedule's); only the parallelism changes. */
+    int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
+                           target set across processes passes its shard's offset, so every target gets
+                           the same draws (and results) as in a single process; 0 otherwise */
 } kin_ik_params;
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,

@@ -161,6 +161,7 @@ struct kin_model {
 };
 
 struct kin_sdf {
+    int device = -1;        // HIP device holding the box tables (current device at creation)
     int32_t n_boxes = 0;
     int32_t n_aabb = 0;     // the first n_aabb boxes are axis-aligned (KAabb table after the KBox array)
     double bc[3] = {0, 0, 0}, bh[3] = {0, 0, 0};  // world-aligned box enclosing every box (broad phase, coll_body)
@@ -173,6 +174,7 @@ struct kin_sdf {
 };
 
 struct kin_plan {
+    int device = -1;  // HIP device holding the staged program (current device at creation); runs must match
     int32_t dtype = KIN_F32;
     int32_t nqcols = 0, rows = 0, ncols = 0, n_q = 0, n_out = 0;
     bool has_jac = false, with_base = false, has_rpy = false;
@@ -717,7 +719,9 @@ struct Stager {
         }
         P.h_steps = host;
         P.n_steps = (int32_t)steps.size();
-        hipError_t e = hipMalloc(&P.d_steps, bytes);
+        hipError_t e = hipGetDevice(&P.device);
+        if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("hipGetDevice: ") + hipGetErrorString(e));
+        e = hipMalloc(&P.d_steps, bytes);
         if (e != hipSuccess) {
             P.d_steps = nullptr;
             return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -778,9 +782,23 @@ int plan_create(const kin_model* m, const kin_plan_desc* d, kin_plan** out) {
 
 bool dev_ptr_ok(const void* p) { return p != nullptr; }
 
+// A plan's program (and its specialised module) lives on the device that was current when it was
+// created; launching it from another device would read that memory through the wrong context.
+int check_device(int owner, const char* fn, const char* what) {
+    int cur = -1;
+    const hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string(fn) + ": hipGetDevice: " + hipGetErrorString(e));
+    if (cur != owner)
+        return set_error(KIN_E_INVALID, std::string(fn) + ": " + what + " lives on HIP device " + std::to_string(owner) +
+                                            " but the current device is " + std::to_string(cur));
+    return KIN_OK;
+}
+
 std::string cache_key(const kin_model* m, const kin_plan_desc& d) {
     std::ostringstream k;
-    k << m->version << '|' << d.dtype << '|' << d.jac_link_id << '|' << d.jac_flags << "|q";
+    int dev = -1;
+    (void)hipGetDevice(&dev);  // one cached plan per device (kin_get_*_batch from several devices)
+    k << dev << '#' << m->version << '|' << d.dtype << '|' << d.jac_link_id << '|' << d.jac_flags << "|q";
     for (int32_t c = 0; c < d.n_q; ++c) k << ',' << d.q_joint_ids[c];
     k << "|o";
     for (int32_t c = 0; c < d.n_out; ++c) k << ',' << d.out_link_ids[c];
@@ -962,6 +980,7 @@ int plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* pos
     if (!p) return bad("null plan");
     if (n < 0) return bad("n < 0");
     if (n == 0) return KIN_OK;
+    if (const int rc = check_device(p->device, fn, "the plan")) return rc;
     const int64_t span = std::min(ta.tile, n);  // configurations along one row of one tile
     if (p->nqcols > 0 && (!dev_ptr_ok(q) || ldq < span)) return bad("bad q / ldq");
     if (p->n_out > 0 && !poses) return bad("null poses");
@@ -1019,6 +1038,7 @@ int specialize_one(kin_plan* p, uint32_t kernels) {
 
 int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
     if (!p) return set_error(KIN_E_INVALID, "kin_plan_specialize: null plan");
+    if (const int rc = check_device(p->device, "kin_plan_specialize", "the plan")) return rc;
     uint32_t applies = 0;
     if (p->is_coll) {
         applies = KIN_SPEC_COLL;
@@ -1136,7 +1156,8 @@ int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* w
             sd->bh[i] = 0.5 * (hi[i] - lo[i]) * (1.0 + 1e-12) + 1e-12;
         }
     }
-    hipError_t e = upload_boxes(&sd->d_f32, bf, af);
+    hipError_t e = hipGetDevice(&sd->device);
+    if (e == hipSuccess) e = upload_boxes(&sd->d_f32, bf, af);
     if (e == hipSuccess) e = upload_boxes(&sd->d_f64, bd, ad);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("kin_sdf_create_boxes: ") + hipGetErrorString(e));
     *out = sd.release();
@@ -1213,6 +1234,7 @@ int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** 
         top->with_base = parts[0]->with_base;
         top->n_q = parts[0]->n_q;
         top->is_coll = true;
+        top->device = parts[0]->device;
         top->n_sph = c->n_spheres;
         top->parts = std::move(parts);
     }
@@ -1259,6 +1281,8 @@ int coll_check(const kin_plan* p, const kin_sdf* sdf, const void* q, int64_t ldq
     if (!p->is_coll) return bad("plan was not made by kin_coll_plan_create");
     if (n < 0) return bad("n < 0");
     if (n == 0) return KIN_OK;
+    if (const int rc = check_device(p->device, fn, "the plan")) return rc;
+    if (const int rc = check_device(sdf->device, fn, "the kin_sdf")) return rc;
     const int64_t span = std::min(ta.tile, n);
     if ((p->nqcols > 0 && (!q || ldq < span)) || (out1 && ld1 < span) || (out2 && ld2 < span))
         return bad("bad pointer / stride");
@@ -1343,12 +1367,14 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
     if (n == 0) return KIN_OK;
     if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
+    if (const int rc = check_device(p->device, "kin_ik_dls_batch", "the plan")) return rc;
     if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0) || prm->restarts < 0)
         return set_error(KIN_E_INVALID, "bad IK parameters");
     if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
         return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
+    if (prm->index_base < 0) return set_error(KIN_E_INVALID, "kin_ik_params.index_base < 0");
     IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-             prm->restarts, prm->seed, prm->lanes};
+             prm->restarts, prm->seed, prm->lanes, prm->index_base};
     // the specialised IK kernels address rows with 32-bit offsets (ldn_soa): every lane offset of a
     // launch chunk plus rows * ld must stay below 2^31 bytes, else the generic kernel runs
     const int64_t esz = p->dtype == KIN_F32 ? 4 : 8;
@@ -1375,6 +1401,7 @@ int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
     if (n == 0) return KIN_OK;
     if (!pts || ldpt < n || !q || ldq < n) return set_error(KIN_E_INVALID, "bad pointer / stride");
+    if (const int rc = check_device(p->device, "kin_point_ik_nakamura_batch", "the plan")) return rc;
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_nakamura<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)pts, ldpt,

@@ -67,7 +67,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     const int64_t resident_waves = (int64_t)cus * (res_env > 0 ? res_env : 8);
     const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
-        at.ibase = s0;
+        at.ibase = a.index_base + s0;
         const int64_t c = std::min(chunk, n - s0);
         const int64_t ng = 64 / G;
         // queue depth: one target per group (no refill) while the batch fills the chip in at most

@@ -97,8 +97,8 @@ __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (
         if (E[8] > E[4 * b]) b = 2;
         T a[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) a[k] = T(0.5) * (E[3 * k + b] + E[3 * b + k]);
-        a[b] = T(0.5) * (E[4 * b] + T(1));
+        for (int k = 0; k < 3; ++k) a[k] = T(0.25) * (E[3 * k + b] + E[3 * b + k]);  // u_k u_b (E = 2uu^T - I)
+        a[b] = T(0.5) * (E[4 * b] + T(1));                                            // u_b^2
         const T nn = sqrt_t(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
 #pragma unroll
         for (int k = 0; k < 3; ++k) w[k] = a[k] / nn * th;
@@ -270,6 +270,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
         if (it >= a.max_iters) {  // only the last attempt gets here
             final_lane = true;
+            it = a.max_iters + 1;  // not converged (kinhip.h: iters > max_iters)
             done = true;
             continue;
         }

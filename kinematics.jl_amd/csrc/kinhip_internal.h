@@ -46,6 +46,7 @@ struct IkArgs {
     int32_t restarts;
     uint64_t seed;
     int32_t lanes;  // 0 auto
+    int64_t index_base;  // global index of target 0 (restart draws)
 };
 
 template <typename T>

@@ -21,7 +21,7 @@ from .collision import (  # noqa: F401
 )
 from .planning import (  # noqa: F401
     ConfigurationConstraint, EqConst, IneqConst, Objective, PoseConstraint, construct_problem,
-    create_straight_trajectory, plan_trajectory,
+    collision_aware_ik, create_straight_trajectory, plan_trajectory,
 )
 
 FETCH_ARM_JOINTS = [

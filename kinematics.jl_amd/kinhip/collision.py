@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib as K
-from .mechanism import Link, Mechanism, _device, _i32, _ld_of, _p, get_transform
+from .mechanism import Link, Mechanism, _device, _i32, _ld_of, _p, _same_device, get_transform
 
 _DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
 _uid = itertools.count()
@@ -154,6 +154,9 @@ class CollisionPlan:
         G = grads if isinstance(grads, torch.Tensor) else (
             torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None)
         Mn = torch.empty(N, dtype=self.dtype, device=dev) if min_dist else None
+        for t, what in ((D, "dists"), (G, "grads")):
+            if t is not None:
+                _same_device(t, Q, what)
         ldd = _ld_of(D.unsqueeze(0), (1, self.n_sph, N), self.dtype) if D is not None else N
         ldg = _ld_of(G, (self.n_sph, self.n_dof, N), self.dtype) if G is not None else N
         st = (stream or torch.cuda.current_stream(dev)).cuda_stream

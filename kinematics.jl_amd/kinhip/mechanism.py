@@ -242,10 +242,7 @@ class Plan:
         d = K.PlanDesc(_DT[dtype], self._q.size, _p(self._q).value, self._o.size, _p(self._o).value,
                        self._jl, self._j.size, _p(self._j).value, flags)
         self._h = C.c_void_p()
-        rc = K.lib().kin_plan_create(m._model, C.byref(d), C.byref(self._h))
-        if rc != K.KIN_OK:
-            msg = K.lib().kin_last_error().decode()
-            raise K.error_class(rc)(msg) if rc in (K.KIN_E_KEY, K.KIN_E_METHOD) else K.KinError(rc, msg)
+        _raise_like_julia(K.lib().kin_plan_create(m._model, C.byref(d), C.byref(self._h)))
         nq, rows, cols = C.c_int32(), C.c_int32(), C.c_int32()
         K.check(K.lib().kin_plan_shape(self._h, C.byref(nq), C.byref(rows), C.byref(cols)))
         self.n_qcols, self.jac_rows, self.jac_cols = nq.value, rows.value, cols.value
@@ -285,6 +282,9 @@ class Plan:
         if jac is None and self._jl:
             alloc = torch.zeros if not self.zero_fill else torch.empty
             jac = alloc((self.jac_cols, self.jac_rows, N), dtype=self.dtype, device=dev)
+        for t, what in ((poses, "poses"), (jac, "jac")):
+            if t is not None:
+                _same_device(t, Q, what)
         ldp = _ld_of(poses, (self.n_out, 12, N), self.dtype) if poses is not None else N
         ldj = _ld_of(jac, (self.jac_cols, self.jac_rows, N), self.dtype) if jac is not None else N
         st = (stream or torch.cuda.current_stream(dev)).cuda_stream
@@ -316,6 +316,7 @@ class Plan:
                 return None, tile, 0
             if tuple(t.shape) != shape or t.dtype != self.dtype or not t.is_cuda or t.stride(3) != 1:
                 raise ValueError(f"tiled output must be a CUDA {self.dtype} tensor of shape {shape}")
+            _same_device(t, Qt, "tiled output")
             a, b = shape[1], shape[2]
             ld = t.stride(2)
             if a > 1 and t.stride(1) != b * ld:
@@ -330,16 +331,19 @@ class Plan:
         return poses, jac
 
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, stream=None):
+               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None):
         """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
-        target running restart attempts side by side (0 auto; results identical for every value)."""
+        target running restart attempts side by side (0 auto; results identical for every value).
+        `index_base`: global index of target 0 for the restart draws (a shard's offset), so a target
+        set sharded over ranks solves exactly as in one process.  iters > max_iters: not converged."""
         N = self._check_q(Q)
         if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
             raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
+        _same_device(targets, Q, "targets")
         iters = torch.empty(N, dtype=torch.int32, device=Q.device)
         err = torch.empty((2, N), dtype=self.dtype, device=Q.device)
         prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
-                         int(restarts), int(seed), int(lanes))
+                         int(restarts), int(seed), int(lanes), int(index_base))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         K.check(K.lib().kin_ik_dls_batch(self._h, C.byref(prm), targets.data_ptr(), N, Q.data_ptr(), Q.stride(0), N,
                                          iters.data_ptr(), err.data_ptr(), N, st))
@@ -349,6 +353,7 @@ class Plan:
         N = self._check_q(Q)
         if points.shape != (3, N) or points.dtype != self.dtype or not points.is_contiguous():
             raise ValueError("points must be a contiguous (3, N) tensor of the plan dtype")
+        _same_device(points, Q, "points")
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         K.check(K.lib().kin_point_ik_nakamura_batch(self._h, points.data_ptr(), N, Q.data_ptr(), Q.stride(0), N, st))
         return Q
@@ -484,6 +489,13 @@ def untiled(Xt: torch.Tensor, n: int) -> torch.Tensor:
     return X.reshape(*X.shape[:-2], -1)[..., :n]
 
 
+def _same_device(t: torch.Tensor, ref: torch.Tensor, what: str):
+    """A device pointer handed to the C-ABI must live on the device of the launch (Q's): a host or
+    other-GPU tensor would reach the kernel as a bad address (a GPU fault, not an error code)."""
+    if not t.is_cuda or t.device != ref.device:
+        raise ValueError(f"{what} must be a CUDA tensor on {ref.device} (got {t.device})")
+
+
 def _ld_of(t: torch.Tensor, shape, dtype) -> int:
     """Leading dimension of a [a][b][ld] SoA output given as a (possibly row-padded) view of shape
     `shape` = (a, b, N): configuration stride 1, rows `ld` apart (the C-ABI's ldp / ldj)."""
@@ -510,7 +522,7 @@ def _single_q(m: Mechanism, dev):
 def get_transform(m: Mechanism, link: Link) -> np.ndarray:
     """World pose (4x4) of ``link`` at the mechanism's current angles (src/algorithm.jl:1-4)."""
     dev = _device()
-    key = ("tf", link.id, len(m.joints))
+    key = ("tf", link.id, len(m.joints), dev.index)
     plan = m.__dict__.setdefault("_single_plans", {}).get(key)
     if plan is None:
         plan = m.plan(m.joints, out_links=[link], dtype=torch.float64)
@@ -524,7 +536,7 @@ def get_transform(m: Mechanism, link: Link) -> np.ndarray:
 def get_jacobian_(m: Mechanism, link: Link, joints, with_rot: bool, mat_out: np.ndarray, rpy_jac=False):
     """``get_jacobian!`` (src/algorithm.jl:83-106): writes relevant columns into mat_out."""
     dev = _device()
-    key = ("jac", link.id, tuple(j.id for j in joints), bool(with_rot), bool(rpy_jac), len(m.joints))
+    key = ("jac", link.id, tuple(j.id for j in joints), bool(with_rot), bool(rpy_jac), len(m.joints), dev.index)
     plans = m.__dict__.setdefault("_single_plans", {})
     plan = plans.get(key)
     ids = list(range(1, len(m.joints) + 1))
@@ -546,18 +558,71 @@ def get_jacobian(m: Mechanism, link: Link, joints, with_rot: bool, rpy_jac=False
     return get_jacobian_(m, link, joints, with_rot, J, rpy_jac=rpy_jac)
 
 
-def get_transform_batch(m: Mechanism, links, joints, Q: torch.Tensor):
-    """Batched get_transform: Q (len(joints)[+3], N) -> poses (len(links), 12, N)."""
-    plan = m.plan(joints, out_links=links, dtype=Q.dtype)
-    return plan.run(Q)[0]
+def get_transform_batch(m: Mechanism, links, joints, Q: torch.Tensor, poses: Optional[torch.Tensor] = None,
+                        stream=None):
+    """Batched get_transform: Q (len(joints)[+3], N) -> poses (len(links), 12, N).  Async.
+
+    Runs through ``kin_get_transform_batch``: the C side keeps one plan per request in the model
+    and drops them when the model changes (``set_joint_angles`` of joints outside `joints`,
+    ``add_new_link``); that drop frees device memory, which synchronises the device once."""
+    m._sync_angles()
+    _check_q_batch(m, joints, Q)
+    N = Q.shape[1]
+    ids = _ids(joints)
+    oids = _ids(links)
+    if poses is None:
+        poses = torch.empty((oids.size, 12, N), dtype=Q.dtype, device=Q.device)
+    _same_device(poses, Q, "poses")
+    ldp = _ld_of(poses, (oids.size, 12, N), Q.dtype)
+    st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+    rc = K.lib().kin_get_transform_batch(m._model, _DT[Q.dtype], ids.size, _p(ids), Q.data_ptr(), Q.stride(0), N,
+                                         oids.size, _p(oids), poses.data_ptr(), ldp, st)
+    _raise_like_julia(rc)
+    return poses
 
 
-def get_jacobian_batch(m: Mechanism, link, joints, Q: torch.Tensor, with_rot=True, rpy_jac=False):
-    """Batched get_transform + get_jacobian: -> (pose (12, N), jac (cols, rows, N))."""
-    plan = m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=with_rot, rpy_jac=rpy_jac,
-                  dtype=Q.dtype)
-    poses, jac = plan.run(Q)
-    return poses[0], jac
+def get_jacobian_batch(m: Mechanism, link, joints, Q: torch.Tensor, with_rot=True, rpy_jac=False, stream=None):
+    """Batched get_transform + get_jacobian (``kin_get_jacobian_batch``, cached per model like
+    get_transform_batch): -> (pose (12, N), jac (cols, rows, N)), irrelevant columns zero.  Async."""
+    m._sync_angles()
+    _check_q_batch(m, joints, Q)
+    N = Q.shape[1]
+    ids = _ids(joints)
+    rows = 6 if with_rot else 3
+    cols = ids.size + (3 if m.with_base else 0)
+    pose = torch.empty((1, 12, N), dtype=Q.dtype, device=Q.device)
+    jac = torch.empty((cols, rows, N), dtype=Q.dtype, device=Q.device)
+    flags = (K.KIN_WITH_ROT if with_rot else 0) | (K.KIN_RPY_JAC if rpy_jac else 0) | K.KIN_ZERO_FILL
+    st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+    rc = K.lib().kin_get_jacobian_batch(m._model, _DT[Q.dtype], link.id, ids.size, _p(ids), flags, Q.data_ptr(),
+                                        Q.stride(0), N, pose.data_ptr(), N, jac.data_ptr(), N, st)
+    _raise_like_julia(rc)
+    return pose[0], jac
+
+
+def _check_q_batch(m: Mechanism, joints, Q: torch.Tensor):
+    if Q.dtype not in _DT:
+        raise TypeError("Q must be torch.float32 or torch.float64")
+    nq = len(joints) + (3 if m.with_base else 0)
+    if not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != nq or Q.stride(1) != 1:
+        raise ValueError(f"Q must be a configuration-contiguous CUDA tensor of shape ({nq}, N)")
+
+
+def _raise_like_julia(rc):
+    if rc != K.KIN_OK:
+        msg = K.lib().kin_last_error().decode()
+        raise K.error_class(rc)(msg) if rc in (K.KIN_E_KEY, K.KIN_E_METHOD) else K.KinError(rc, msg)
+
+
+def _cached_plan(m: Mechanism, key, make):
+    """Per-mechanism cache of the single-configuration convenience plans, keyed by the request, the
+    mechanism state they were staged with (angles of non-batched joints, tree size) and the device."""
+    key = key + (m.angles.tobytes(), len(m.joints), torch.cuda.current_device())
+    plans = m.__dict__.setdefault("_single_plans", {})
+    p = plans.get(key)
+    if p is None:
+        p = plans[key] = make()
+    return p
 
 
 def translation(T) -> np.ndarray:
@@ -594,29 +659,66 @@ def rpy(T) -> np.ndarray:
 def point_inverse_kinematics_nakamura(m: Mechanism, link: Link, joints, point_desired) -> np.ndarray:
     """src/algorithm.jl:116-131 on the GPU (batch of one); returns the angles."""
     dev = _device()
-    plan = m.plan(joints, jac_link=link, jac_joints=joints, with_rot=False, dtype=torch.float64)
+    m._sync_angles()
+    plan = _cached_plan(m, ("nakamura", link.id, tuple(j.id for j in joints)),
+                        lambda: m.plan(joints, jac_link=link, jac_joints=joints, with_rot=False, dtype=torch.float64))
     Q = torch.tensor([m.angles[j.id - 1] for j in joints], dtype=torch.float64, device=dev).reshape(-1, 1)
     pts = torch.tensor(np.asarray(point_desired, np.float64), device=dev).reshape(3, 1).contiguous()
     plan.point_ik_nakamura(pts, Q)
     return Q[:, 0].cpu().numpy()
 
 
-def inverse_kinematics_(m: Mechanism, link: Link, joints, target_pose, ftol=1e-5, with_rot=True, max_iters=64,
-                        lam=1e-2, max_step=0.5):
-    """``inverse_kinematics!`` (src/inverse_kinematics.jl:23-30) via the batched DLS kernel.
+def inverse_kinematics_(m: Mechanism, link: Link, joints, target_pose, sscc=None, sdf=None, use_bistage=True,
+                        ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2, max_step=0.5):
+    """``inverse_kinematics!`` (src/inverse_kinematics.jl:1-30) -> (q, status); sets the mechanism's angles.
 
-    Returns (q, status) with status ``:FTOL_REACHED`` when converged (position
-    and rotation error below 1e-3, the reference test's acceptance) else
-    ``:MAXEVAL_REACHED``.  Sets the mechanism's angles to the solution.
+    Without ``sscc`` / ``sdf`` (src/inverse_kinematics.jl:23-30): the DLS kernel, one iteration per
+    launch, stopped by the reference's ``ftol_abs`` rule (NLopt stops when one step changes the
+    objective by less than ftol): objective = |dp|^2 + |rot err|^2 (the DLS residual, an axis-angle
+    error where the reference uses rpy differences).  Status ``:FTOL_REACHED`` when that rule
+    stopped it, ``:MAXEVAL_REACHED`` after ``max_iters`` steps.
+
+    With ``sscc`` and ``sdf`` (src/inverse_kinematics.jl:1-21): the collision-aware form.  Stage 1
+    (``use_bistage``) is the collision-free solve above; stage 2 minimises the reference's objective
+    (sum of squared position + rpy differences, gradient -2 J_rpy^T diff) subject to the sphere
+    distances of ``IneqConst(sscc, joints, sdf, 1, 0.02)`` >= -1e-8 and the joint limits, with SLSQP
+    on the host (SciPy's; the reference uses NLopt's LD_SLSQP) and every evaluation on the GPU
+    (kin_pose_const_batch, kin_ineq_const_batch).  Status ``:FTOL_REACHED`` when SLSQP met its
+    ftol convergence test, else ``:MAXEVAL_REACHED`` / ``:FAILURE``.
     """
+    if (sscc is None) != (sdf is None):
+        raise TypeError("inverse_kinematics_: pass both sscc and sdf (collision-aware form) or neither")
+    if sscc is not None:
+        from .planning import collision_aware_ik
+        return collision_aware_ik(m, link, joints, target_pose, sscc, sdf, use_bistage=use_bistage, ftol=ftol,
+                                  with_rot=with_rot, max_iters=max_iters, lam=lam, max_step=max_step)
+    return _dls_ik_ftol(m, link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step)
+
+
+def _dls_ik_ftol(m: Mechanism, link: Link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step):
     dev = _device()
-    plan = m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=True, dtype=torch.float64)
+    m._sync_angles()
+    plan = _cached_plan(m, ("ik", link.id, tuple(j.id for j in joints)),
+                        lambda: m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=True,
+                                       dtype=torch.float64))
     Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
     T = np.asarray(target_pose, np.float64)
     tgt = torch.tensor(T[:3, :4].T.reshape(12), device=dev).reshape(12, 1).contiguous()
-    Q, iters, err = plan.ik_dls(tgt, Q, max_iters=max_iters, lam=lam, tol_pos=1e-3 * 0.1, tol_rot=1e-3 * 0.1,
-                                max_step=max_step, with_rot=with_rot)
+    kw = dict(lam=lam, tol_pos=0.0, tol_rot=0.0, max_step=max_step, with_rot=with_rot)
+
+    def objective(max_it):  # max_it = 0: evaluate only; 1: one DLS step, then evaluate
+        _, _, err = plan.ik_dls(tgt, Q, max_iters=max_it, **kw)
+        e = err[:, 0].cpu().numpy()
+        return float(e[0] ** 2 + e[1] ** 2)
+
+    f = objective(0)
+    status = ":MAXEVAL_REACHED"
+    for _ in range(int(max_iters)):
+        f_new = objective(1)
+        if abs(f - f_new) < ftol:
+            status = ":FTOL_REACHED"
+            break
+        f = f_new
     q = Q[:, 0].cpu().numpy()
     m.set_joint_angles(joints, q)
-    ok = int(iters[0].item()) < max_iters
-    return q, (":FTOL_REACHED" if ok else ":MAXEVAL_REACHED")
+    return q, status

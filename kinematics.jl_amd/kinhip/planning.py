@@ -13,9 +13,10 @@ ONE batched launch over all waypoints (of one or many trajectories):
 The optimiser stays on the host, as the reference's does: ``Objective``,
 ``ConfigurationConstraint``, ``EqConst`` are small host-side assemblies and
 ``plan_trajectory`` drives SciPy's SLSQP (the reference's ``solver=:SCIPY``
-path).  NLopt and Ipopt are not available offline; ``solver="NLOPT"`` runs the
-same SLSQP algorithm (Kraft's, which NLopt's LD_SLSQP also wraps) with NLopt's
-bounds and ``ftol_abs`` semantics and reports NLopt-style status symbols.
+path).  NLopt and Ipopt are not installed, so ``solver=:NLOPT`` / ``:IPOPT`` are
+refused; ``solver="SLSQP_BOUNDED"`` (the default) is SciPy's SLSQP with the
+joint-limit bounds the reference's NLopt path sets (src/planning.jl:364-369) --
+SciPy's implementation, not NLopt's -- and reports its status as a symbol.
 """
 from __future__ import annotations
 
@@ -27,7 +28,7 @@ import torch
 
 from . import _lib as K
 from .collision import SweptSphereCollisionChecker, UnionSDF
-from .mechanism import Link, Mechanism, _device
+from .mechanism import Link, Mechanism, _device, _same_device
 
 _DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
 
@@ -157,6 +158,7 @@ class PoseConstraint(PartialConstraint):
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
         if targets.dtype != self.dtype or targets.shape != (12, N) or targets.stride(1) != 1:
             raise ValueError("targets must be (12, N) in the plan dtype")
+        _same_device(targets, Q, "targets")
         P = torch.empty((12, N), dtype=self.dtype, device=Q.device)
         V = torch.empty((dim, N), dtype=self.dtype, device=Q.device)
         J = torch.empty((self.n_dof, dim, N), dtype=self.dtype, device=Q.device)  # zero-filled plan
@@ -222,14 +224,21 @@ def construct_problem(sscc, joints, sdf, q_start, q_goal, n_wp, n_dof, margin, p
 
 
 def plan_trajectory(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, q_start, q_goal, n_wp: int,
-                    margin=2e-2, partial_consts=(), ftol_abs=1e-3, solver="NLOPT", maxiter=200):
-    """src/planning.jl:332-401 -> (q_seq [n_dof, n_wp], status).  Constraint evaluations on the GPU."""
+                    margin=2e-2, partial_consts=(), ftol_abs=1e-3, solver="SLSQP_BOUNDED", maxiter=200):
+    """src/planning.jl:332-401 -> (q_seq [n_dof, n_wp], status).  Constraint evaluations on the GPU.
+
+    ``solver``: "SLSQP_BOUNDED" (SciPy SLSQP + joint-limit bounds; status ``:SUCCESS`` /
+    ``:MAXEVAL_REACHED`` / ``:FAILURE``) or "SCIPY" (the reference's :SCIPY path: no bounds, returns
+    SciPy's result).  "NLOPT" and "IPOPT" raise: those libraries are not installed."""
     from scipy.optimize import minimize
     from .collision import compute_coll_dists
 
     solver = str(solver).lstrip(":").upper()
-    if solver not in ("NLOPT", "SCIPY"):
-        raise ValueError(f"solver {solver!r} is not available (NLopt-compatible SLSQP and SCIPY are)")
+    if solver in ("NLOPT", "IPOPT"):
+        raise ValueError(f"solver :{solver} needs a library that is not installed; use 'SLSQP_BOUNDED' "
+                         "(SciPy SLSQP with the joint-limit bounds) or 'SCIPY'")
+    if solver not in ("SLSQP_BOUNDED", "SCIPY"):
+        raise ValueError(f"unknown solver {solver!r}")
     m = sscc.mech
     n_dof = len(joints) + (3 if m.with_base else 0)
     assert len(q_start) == n_dof and len(q_goal) == n_dof
@@ -255,7 +264,7 @@ def plan_trajectory(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, q_
     grad = np.zeros(n_whole)
     cons = [{"type": "ineq", "fun": g_val, "jac": g_jac}, {"type": "eq", "fun": h_val, "jac": h_jac}]
     bounds = None
-    if solver == "NLOPT":
+    if solver == "SLSQP_BOUNDED":
         lo = [j.lower_limit for j in joints] + ([-np.inf] * 3 if m.with_base else [])
         hi = [j.upper_limit for j in joints] + ([np.inf] * 3 if m.with_base else [])
         bounds = list(zip(lo * n_wp, hi * n_wp))
@@ -264,5 +273,62 @@ def plan_trajectory(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, q_
     q_seq = res.x.reshape(n_wp, n_dof).T
     if solver == "SCIPY":
         return q_seq, res
-    status = ":FTOL_REACHED" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")
+    status = ":SUCCESS" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")
     return q_seq, status
+
+
+def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: SweptSphereCollisionChecker,
+                       sdf: UnionSDF, use_bistage=True, ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2,
+                       max_step=0.5, margin=0.02):
+    """``inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)`` (src/inverse_kinematics.jl:1-21);
+    see ``kinhip.inverse_kinematics_``.  -> (q, status); sets the mechanism's angles."""
+    from scipy.optimize import minimize
+    from .mechanism import _dls_ik_ftol
+
+    if use_bistage:  # stage 1: the collision-free problem seeds stage 2 (src/inverse_kinematics.jl:8-13)
+        _dls_ik_ftol(m, link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step)
+    n_dof = len(joints) + (3 if m.with_base else 0)
+    T = np.asarray(target_pose, np.float64).reshape(4, 4)
+    # objective: PoseConstraint's residual [p - p*; rpy - rpy*] and its rpy Jacobian on the GPU
+    pc = PoseConstraint(1, n_dof, link, T, with_rot, m, joints, dtype=torch.float64)
+    # src/inverse_kinematics.jl:16 (a checker without spheres has no constraints: the reference's own
+    # PR2 test builds one, test/test_inverse_kinematics.jl:63, with an un-iterated generator)
+    G = IneqConst(sscc, joints, sdf, 1, margin, dtype=torch.float64) if sscc.sphere_links else None
+    dev = _device()
+    tg = torch.tensor(np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]]), dtype=torch.float64,
+                      device=dev).reshape(12, 1)
+    rel = np.array([m.is_relevant(j, link) for j in joints] + [True] * (n_dof - len(joints)))
+
+    def pose_eval(x):
+        Q = torch.tensor(np.asarray(x, np.float64), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+        V, J, _ = pc.eval_batch(0, Q, tg)
+        v = V[:, 0].cpu().numpy()               # now - target
+        Jh = J[:, :, 0].cpu().numpy() * rel[:, None]  # [n_dof, dim]
+        return float(np.dot(v, v)), 2.0 * Jh @ v  # f = sum(diff.^2), grad = -2 J^T diff
+
+    def cached(fn):
+        last = {}
+
+        def ev(x):
+            k = np.asarray(x, np.float64).tobytes()
+            if last.get("k") != k:
+                last.update(k=k, r=fn(x))
+            return last["r"]
+        return ev
+
+    fo = cached(pose_eval)
+
+    def g_eval(x):
+        G(x, G.val_vec, G.jac_mat)
+        return G.val_vec + 1e-8, G.jac_mat.T.copy()  # nloptize(G) <= 1e-8  <=>  dist - margin >= -1e-8
+    go = cached(g_eval)
+    lo = [j.lower_limit for j in joints] + [-np.inf] * (n_dof - len(joints))
+    hi = [j.upper_limit for j in joints] + [np.inf] * (n_dof - len(joints))
+    x0 = np.clip(m.get_joint_angles(joints), lo, hi)
+    cons = [{"type": "ineq", "fun": lambda x: go(x)[0], "jac": lambda x: go(x)[1]}] if G is not None else []
+    res = minimize(lambda x: fo(x)[0], x0, jac=lambda x: fo(x)[1], method="SLSQP", bounds=list(zip(lo, hi)),
+                   constraints=cons, options={"ftol": ftol, "maxiter": max_iters})
+    q = np.asarray(res.x, np.float64)
+    m.set_joint_angles(joints, q)
+    status = ":FTOL_REACHED" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")
+    return q, status

@@ -614,11 +614,19 @@ static void rot_error(const tf_t* tgt, const tf_t* now, double w[3]) {
         if (E[4] > E[b * 4]) b = 1;
         if (E[8] > E[b * 4]) b = 2;
         double a[3];
-        for (int i = 0; i < 3; ++i) a[i] = 0.5 * (E[i + 3 * b] + E[b + 3 * i]);
-        a[b] = 0.5 * (E[b * 4] + 1.0);
+        for (int i = 0; i < 3; ++i) a[i] = 0.25 * (E[i + 3 * b] + E[b + 3 * i]); /* u_i u_b (E = 2uu^T - I) */
+        a[b] = 0.5 * (E[b * 4] + 1.0);                                            /* u_b^2 */
         double nn = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
         for (int i = 0; i < 3; ++i) w[i] = a[i] / nn * th;
     }
+}
+
+/* exported for the known-answer test of the angle ~ pi branch (tests/test_oracle.py) */
+void or_rot_error(const double* tgt16, const double* now16, double* w3) {
+    tf_t a, b;
+    memcpy(a.m, tgt16, sizeof a.m);
+    memcpy(b.m, now16, sizeof b.m);
+    rot_error(&a, &b, w3);
 }
 
 /* Cholesky solve of symmetric positive definite A (n x n, col-major), in place on b */
@@ -733,6 +741,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                 }
             }
             for (int32_t c = 0; c < ndof; ++c) q[c * ldq + i] = a[c];
+            if (!(ep < prm->tol_pos && er < prm->tol_rot)) it = prm->max_iters + 1; /* not converged */
             if (iters_out) iters_out[i] = it;
             if (err_out) { err_out[i] = ep; err_out[n + i] = er; }
         }

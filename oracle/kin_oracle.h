@@ -113,6 +113,8 @@ typedef struct {
 } or_ik_params;
 /* the restart re-seed draw in [0, 1) shared by the oracle and the GPU kernel */
 double or_ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col);
+/* log(Rt R^T) as a world rotation vector (the IK's rotation error); 4x4 column-major inputs */
+void or_rot_error(const double* tgt16, const double* now16, double* w3);
 void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, int32_t n_q,
                      const int32_t* q_joint_ids, int32_t link_id, const double* target, int64_t ldt,
                      const or_ik_params* prm, int32_t* iters_out, double* err_out, int32_t n_threads);

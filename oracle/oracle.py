@@ -187,6 +187,7 @@ def lib():
         L.or_fk_jac_batch.argtypes = [P, I64, P, I64, I32, P, I32, I32, P, I32, I32, I32, P, I64, P, I64, I32]
         L.or_point_ik_nakamura_batch.argtypes = [P, I64, P, I64, I32, P, I32, P, I64, I32]
         L.or_ik_dls_batch.argtypes = [P, I64, P, I64, I32, P, I32, P, I64, P, P, P, I32]
+        L.or_rot_error.argtypes = [P, P, P]
         L.or_sdf_create.restype = P
         L.or_sdf_create.argtypes = [I32, P, P]
         L.or_sdf_destroy.argtypes = [P]
@@ -338,6 +339,14 @@ class OracleMech:
         lib().or_ik_dls_batch(self._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt), tgt.shape[1],
                               C.byref(prm), _p(it), _p(err), n_threads)
         return q, it, err
+
+
+def rot_error(T_target, T_now):
+    """The DLS IK's rotation error: log(R* R^T) as a world rotation vector (or_rot_error)."""
+    a, b = tf_colmajor(T_target), tf_colmajor(T_now)
+    w = np.zeros(3)
+    lib().or_rot_error(_p(a), _p(b), _p(w))
+    return w
 
 
 def rpy(T):

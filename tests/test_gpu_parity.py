@@ -2,7 +2,9 @@
 
 Tolerances (stated per BASELINE north star: poses / Jacobian entries within 1e-6 absolute):
   fp64 kernels: 1e-9 absolute vs the oracle (observed ~1e-15)
-  fp32 kernels: 2e-5 absolute vs the oracle evaluated at the fp32-rounded angles
+  fp32 kernels: 1e-6 absolute vs the oracle evaluated at the fp32-rounded angles (the north star;
+    observed ~4e-7).  Angles here are drawn in [-2.5, 2.5], beyond some limits; rpy-Jacobian rows
+    (which divide by cos(pitch)) get 20x.  tests/test_gpu_fp32_gate.py gates the bench's exact path.
 """
 import json
 
@@ -17,7 +19,7 @@ import kinhip
 
 pytestmark = pytest.mark.gpu
 
-TOL = {torch.float64: 1e-9, torch.float32: 2e-5}
+TOL = {torch.float64: 1e-9, torch.float32: 1e-6}
 
 
 @pytest.fixture(scope="module")
@@ -124,8 +126,12 @@ def test_fk_jac_vs_oracle(dev, fetch_tree, dtype, with_base, rpy_jac):
     np.testing.assert_allclose(pose.double().cpu().numpy(), ps, atol=TOL[dtype])
     jg = jac.double().cpu().numpy()
     if rpy_jac:  # rpy rows blow up at pitch = +-pi/2; compare where cos(pitch) is not tiny
-        ok = np.sqrt(ps[0] ** 2 + ps[1] ** 2) > 0.05
-        np.testing.assert_allclose(jg[:, :, ok], js[:, :, ok], atol=TOL[dtype] * 20)
+        c = np.sqrt(ps[0] ** 2 + ps[1] ** 2)  # cos(pitch)
+        ok = c > 0.05
+        np.testing.assert_allclose(jg[:, :3], js[:, :3], atol=TOL[dtype])
+        # rpy rates: the ZYX rate map carries 1/cos(pitch) and its rounding 1/cos^2 (<= 400x here)
+        err = np.abs(jg[:, 3:, ok] - js[:, 3:, ok])
+        assert np.all(err <= TOL[dtype] / c[ok] ** 2), float((err * c[ok] ** 2).max())
     else:
         np.testing.assert_allclose(jg, js, atol=TOL[dtype])
 
@@ -462,23 +468,27 @@ def test_ik_dls_acceptance(dev, fetch_tree, dtype):
     Q = torch.zeros((8, N), dtype=dtype, device=dev)
     # axis-angle tolerance 2e-4: the reference's rpy criterion (1e-3) amplifies rotation
     # errors by up to 1/cos(pitch); it is checked below where |cos(pitch)| > 0.2 (factor <= 5)
+    # the bench's solver settings (config 4: 64 iterations incl. 3 seeded restarts)
     Q, it, err = plan.ik_dls(torch.tensor(tgt, dtype=dtype, device=dev).contiguous(), Q, max_iters=64,
-                             tol_rot=2e-4)
+                             restarts=3, seed=0, tol_rot=2e-4)
     it = it.cpu().numpy()
-    conv = it < 64
-    assert conv.mean() > 0.5, conv.mean()
+    conv = it <= 64  # kinhip.h: max_iters + 1 <=> no attempt converged
+    assert conv.mean() >= 0.99, conv.mean()
     q = Q.double().cpu().numpy()
     got = om.fk_batch(q, ids, [gl.id])[0]
     dp = np.linalg.norm(got[9:] - tgt[9:], axis=0)
     assert np.all(dp[conv] < 1e-3)
-    for k in np.nonzero(conv)[0][:200]:
+    n_rpy = 0
+    for k in np.nonzero(conv)[0]:  # every converged target
         Ta, Tt = np.eye(4), np.eye(4)
         Ta[:3, :4] = got[:, k].reshape(4, 3).T
         Tt[:3, :4] = tgt[:, k].reshape(4, 3).T
-        d = O.rpy(Ta) - O.rpy(Tt)
-        d = (d + np.pi) % (2 * np.pi) - np.pi
         if abs(np.cos(O.rpy(Tt)[1])) > 0.2:
-            assert np.all(np.abs(d) < 1e-3)
+            d = O.rpy(Ta) - O.rpy(Tt)
+            d = (d + np.pi) % (2 * np.pi) - np.pi
+            assert np.all(np.abs(d) < 1e-3), (k, d)
+            n_rpy += 1
+    assert n_rpy > 0.9 * conv.sum()
     lo = np.array([j.lower_limit for j in arm])
     hi = np.array([j.upper_limit for j in arm])
     tol = 1e-6 if dtype == torch.float32 else 0
@@ -605,9 +615,9 @@ def test_ik_launch_chunk_boundary(dev):
     Q, it, err = plan.ik_dls(tgt, torch.zeros((8, N), dtype=torch.float32, device=dev), max_iters=64, restarts=3)
     idx = torch.cat([torch.arange(0, 256), torch.arange((1 << 24) - 512, (1 << 24) + 512),
                      torch.arange(N - 256, N)]).to(dev)
-    ok = it[idx] < 64
+    ok = it[idx] <= 64
     assert float(ok.float().mean()) > 0.98
-    assert float((it < 64).float().mean()) > 0.99
+    assert float((it <= 64).float().mean()) > 0.99
     P = fk.run(Q[:, idx].contiguous())[0][0]
     dp = (P[9:12] - tgt[9:12, idx]).norm(dim=0)
     assert float(dp[ok].max()) < 2e-3

@@ -194,3 +194,50 @@ def test_ik_objective_gradient(fetch):
         b[i] += eps
         f1, _ = m.ik_objective(gl, ids, T, b)
         assert abs((f1 - f0) / eps - g[i]) < 1e-4
+
+
+def _axis_angle(u, th):
+    u = np.asarray(u, np.float64) / np.linalg.norm(u)
+    K = np.array([[0, -u[2], u[1]], [u[2], 0, -u[0]], [-u[1], u[0], 0]])
+    T = np.eye(4)
+    T[:3, :3] = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+    return T
+
+
+@pytest.mark.parametrize("u", [(1, 1, 0), (1, 0, 0), (0, 1, 1), (1, 2, 3), (-2, 1, 0.5)])
+def test_rot_error_pi_branch(u):
+    """The IK's rotation error at a pi rotation (sin ~ 0, cos < 0 branch) returns pi * u for a
+    rotation about any axis, not only coordinate axes (E = 2uu^T - I: off-diagonals are 2 u_k u_b)."""
+    R0 = _axis_angle((0.3, -0.2, 0.9), 0.7)
+    Rt = _axis_angle(u, np.pi) @ R0  # target = Rot(u, pi) * current
+    w = O.rot_error(Rt, R0)
+    un = np.asarray(u, np.float64) / np.linalg.norm(u)
+    ok = min(np.abs(w - np.pi * un).max(), np.abs(w + np.pi * un).max())  # +-u is the same rotation
+    assert ok < 1e-6, (w, np.pi * un)
+
+
+def test_rot_error_generic_angles():
+    R0 = _axis_angle((0.1, 0.5, -0.4), 1.1)
+    for th in (1e-3, 0.5, 2.0, 3.1):
+        u = np.array([0.2, -0.7, 0.4])
+        w = O.rot_error(_axis_angle(u, th) @ R0, R0)
+        np.testing.assert_allclose(w, th * u / np.linalg.norm(u), atol=1e-9)
+
+
+def test_ik_iters_contract(fetch):
+    """kinhip.h: iters <= max_iters iff converged; a target that converges at exactly max_iters reports
+    max_iters, a failure max_iters + 1."""
+    ids = [fetch.joint_id(n) for n in ARM]
+    gl = fetch.link_id("gripper_link")
+    m = O.OracleMech(fetch)
+    T = np.eye(4)
+    T[:3, 3] = [0.3, -0.4, 1.2]
+    tgt = T[:3, :4].T.reshape(12, 1)
+    q, it, err = m.ik_dls_batch(np.zeros((8, 1)), ids, gl, tgt, max_iters=200, tol_pos=1e-4, tol_rot=1e-4)
+    k = int(it[0])
+    assert k <= 200 and err[0, 0] < 1e-4
+    _, it2, err2 = m.ik_dls_batch(np.zeros((8, 1)), ids, gl, tgt, max_iters=k, tol_pos=1e-4, tol_rot=1e-4)
+    assert int(it2[0]) == k and err2[0, 0] < 1e-4  # converged exactly at max_iters
+    _, it3, err3 = m.ik_dls_batch(np.zeros((8, 1)), ids, gl, tgt, max_iters=k - 1, tol_pos=1e-4, tol_rot=1e-4)
+    assert int(it3[0]) == k  # (k - 1) + 1: not converged
+    assert not (err3[0, 0] < 1e-4 and err3[1, 0] < 1e-4)

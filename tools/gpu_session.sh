@@ -15,7 +15,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
