@@ -325,9 +325,13 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
     lo = [j.lower_limit for j in joints] + [-np.inf] * (n_dof - len(joints))
     hi = [j.upper_limit for j in joints] + [np.inf] * (n_dof - len(joints))
     x0 = np.clip(m.get_joint_angles(joints), lo, hi)
+    # SciPy's SLSQP stops on |f - f_prev| < ftol once feasible.  Stage 2 starts at the stage-1 optimum
+    # (f ~ 0, infeasible) and met that test with the pose still ~sqrt(ftol) off (1e-3 at ftol 1e-5:
+    # tools/cik_probe.py); NLopt reaches its ftol_abs stop after the quadratic tail.  Stage 2 therefore
+    # runs at ftol^2, i.e. the same ftol on the residual norm instead of its square.
     cons = [{"type": "ineq", "fun": lambda x: go(x)[0], "jac": lambda x: go(x)[1]}] if G is not None else []
     res = minimize(lambda x: fo(x)[0], x0, jac=lambda x: fo(x)[1], method="SLSQP", bounds=list(zip(lo, hi)),
-                   constraints=cons, options={"ftol": ftol, "maxiter": max_iters})
+                   constraints=cons, options={"ftol": ftol * ftol, "maxiter": max_iters})
     q = np.asarray(res.x, np.float64)
     m.set_joint_angles(joints, q)
     status = ":FTOL_REACHED" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")
