@@ -379,15 +379,36 @@ def _copy_bw(dev, nbytes=1 << 31):
     return gbs
 
 
-def _pmc_traffic(workload):
+def _pmc_traffic(workload, fname="pmc_fk_jac_f32.json"):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), if present."""
-    p = os.path.join(ROOT, "profiles", "pmc_fk_jac_f32.json")
+    p = os.path.join(ROOT, "profiles", fname)
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
         if d.get("workload") == workload:
             return d.get("hbm_bytes_per_launch")
     return None
+
+
+def _cold_leg(leg, n, stream, bytes_per_eval, reps=10):
+    """One launch at a time after a 1 GiB read (torch sum) has evicted the Infinity Cache: the
+    launch's own HIP events bracket it alone (the read is outside them)."""
+    plan, Qt, P, J = leg
+    scrub = torch.ones(1 << 28, dtype=torch.float32, device=Qt.device)
+    e = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    with torch.cuda.stream(stream):
+        plan.run_tiled(Qt, n, P, J, stream=stream)
+        for e0, e1 in e:
+            scrub.sum()
+            e0.record(stream)
+            plan.run_tiled(Qt, n, P, J, stream=stream)
+            e1.record(stream)
+    torch.cuda.synchronize()
+    t = sum(a.elapsed_time(b) for a, b in e) / reps / 1e3
+    ach = bytes_per_eval * n / t / 1e9
+    del scrub, plan, Qt, P, J
+    return {"avg_launch_us": t * 1e6, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+            "method": "each launch after a 1 GiB read of another buffer (Infinity Cache evicted), 10 launches"}
 
 
 def main():
@@ -496,8 +517,26 @@ def main():
                                    f"({args.tile}, rows, N/{args.tile}))")
     else:
         out["config"]["layout"] = f"plain SoA (kin_plan_run), rows padded to ld = N + {args.row_pad}"
+    out["roofline"]["traffic_source"] = ("profiles/pmc_fk_jac_f32.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this "
+                                         "workload (2*FETCH_SIZE + WRITE_SIZE, gfx950), committed with the round's "
+                                         "profiles" if traffic else None)
     if args.extras:
         out["roofline"]["torch_copy_GBs"] = _copy_bw(dev)  # context: torch device-to-device copy rate
+        # The 2^20 working set (q + outputs, 285 MB) is about the 256 MiB Infinity Cache, so back-to-back
+        # launches find part of the previous launch's lines on die.  Two checks beside the headline:
+        # the same launch after a 1 GiB read has evicted the cache (cold), and batches 4x and 16x the
+        # Infinity Cache, where nothing survives between launches.
+        if args.layout == "tiled":
+            out["roofline"]["cold_cache"] = _cold_leg(leg_tiled(torch.float32, True, [gl], args.tile), N, stream,
+                                                      bytes_per_eval)
+            big = {}
+            for lg, k_s in ((22, 10), (24, 5)):
+                w_b, d_b = timed_leg(torch.float32, True, [gl], args.layout, n=1 << lg, steps=k_s, warmup=2)
+                ach = bytes_per_eval * (1 << lg) / (d_b / k_s) / 1e9
+                big[f"2^{lg}"] = {"evals_per_s": (1 << lg) * ws * k_s / w_b, "avg_launch_us": d_b / k_s * 1e6,
+                                  "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                                  "working_set_MB": bytes_per_eval * (1 << lg) / 1e6}
+            out["roofline"]["large_batches"] = big
     if args.extras and headline_spec:
         # the same workload through the most literal form of the API: generic kernel (no run-time
         # compilation), plain column-major rows (padded ld) -- kin_plan_run as a Julia caller would
@@ -543,8 +582,15 @@ def main():
         # run and is 10-13% faster here than plain rows, fk_jac_f32_layouts *_f64)
         lay64 = "tile%d" % (args.tile // 2) if args.layout64 == "tiled" else "soa"  # same bytes per tile row
         w64, d64 = timed_leg(torch.float64, True, [gl], lay64, steps=k2, warmup=3)
+        a64 = 544 * N / (d64 / k2) / 1e9
         out["fp64_fk_jac"] = {"value": N * ws * k2 / w64, "unit": "evals/s", "avg_launch_us": d64 / k2 * 1e6,
-                              "achieved_GBs": 544 * N / (d64 / k2) / 1e9, "layout": lay64}
+                              "achieved_GBs": a64, "layout": lay64,
+                              "roofline": {"bound": "hbm", "achieved": a64, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                           "frac": a64 / HBM_PEAK_GBS,
+                                           "traffic": _pmc_traffic("fkjac64ts", "pmc_fk_jac_f64.json"),
+                                           "kernel": "kinhip_jit_fk_f64_<program hash>" if args.spec else
+                                           "k_fk<double, 8>", "algorithmic_bytes_per_eval": 544,
+                                           "working_set_MB": 544 * N / 1e6}}
         links = [m.find_link(n) for n in EXAMPLE_LINKS]
         w2, d2 = timed_leg(torch.float64, False, links, lay64, steps=k2, warmup=3)
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,

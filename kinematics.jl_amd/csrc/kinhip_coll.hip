@@ -14,7 +14,8 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
                                               const CollArgs a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                               T* __restrict__ dists, int64_t ldd, T* __restrict__ grads,
                                               int64_t ldg, T* __restrict__ min_dist, const Tiling tl) {
-    coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem);
 }
 
 }  // namespace
@@ -28,6 +29,8 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
     Tiling tl{tiled ? (uint32_t)(ta.tile / 256) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, ta.tsm};
+    // distances + gradients: the union's boxes in LDS (coll_body, kCollLdsBoxes)
+    const size_t lds = grads && a.n_boxes <= kCollLdsBoxes ? (size_t)a.n_boxes * sizeof(KBox<T>) : 0;
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         const int64_t c = std::min(chunk, n - s0);
         const dim3 grid(grid_of(c, 256)), block(256);
@@ -42,14 +45,14 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc,
                             (void*)&ldd, (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tl};
             const hipError_t e =
-                hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+                hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, (unsigned)lds, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }
 #define KIN_CO_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
+        hipLaunchKernelGGL((k_coll<T, MA, false>), grid, block, lds, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
 #define KIN_COG_LAUNCH(MA) \
-        hipLaunchKernelGGL((k_coll<T, MA, true>), grid, block, 0, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
+        hipLaunchKernelGGL((k_coll<T, MA, true>), grid, block, lds, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl)
         if (grads) {
             KIN_MAXA_DISPATCH(g.maxA, KIN_COG_LAUNCH)
         } else {

@@ -37,9 +37,17 @@ __device__ __forceinline__ double signed_sqrt(double k) { return copysign(sqrt(f
 #ifndef KINHIP_AABB_UNROLL
 #define KINHIP_AABB_UNROLL 2
 #endif
+// Boxes copied to LDS at kernel start (distances + gradients): the argmin box of every sphere is
+// a per-lane (divergent) record, and gathering it from global memory puts a vector load behind
+// the sphere's stores -- its s_waitcnt vmcnt then waits for every store the wave has issued, once
+// per sphere.  An LDS gather is counted apart from the stores.  Up to kCollLdsBoxes boxes (4 KiB
+// fp32); larger unions gather from global memory.
+constexpr int kCollLdsBoxes = 64;
+
 template <typename T, bool GRAD>
 __device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
-                                       int nb, T px, T py, T pz, T (&gw)[3]) {
+                                       int nb, T px, T py, T pz, T (&gw)[3], const unsigned char* smem,
+                                       bool use_lds) {
     T best = T(INFINITY);
     int bk = 0;
     // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
@@ -75,7 +83,19 @@ __device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const 
     }
     const T d = signed_sqrt(best);
     if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
-        const KBox<T>& b = boxes[bk];
+        KBox<T> b;
+        if (use_lds) {
+            const KBox<T>* lb = reinterpret_cast<const KBox<T>*>(smem);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) b.inv[i] = lb[bk].inv[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) b.half[i] = lb[bk].half[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) b.inv[i] = boxes[bk].inv[i];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) b.half[i] = boxes[bk].half[i];
+        }
         T l[3], q[3], gl[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -106,7 +126,8 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              int na, int nb, T trunc, T offs, bool broad, const T (&bnd)[6],
                                              const T (&rm)[MAXA][3], const T (&rz)[MAXA][3], T bx, T by,
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
-                                             T* __restrict__ grads, int64_t ldg, T& dmin) {
+                                             T* __restrict__ grads, int64_t ldg, T& dmin,
+                                             const unsigned char* smem, bool use_lds) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
     for (int k = k0; k < k1; ++k) {
         const KSphere<T>& sp = sph[k];
@@ -135,7 +156,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
             d = trunc;
             cut = true;
         } else {
-            d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g) - sp.r;
+            d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g, smem, use_lds) - sp.r;
             cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
             if (cut) d = trunc;
         }
@@ -187,7 +208,16 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
                                           const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                           const CollArgs& a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                           T* __restrict__ dists, int64_t ldd, T* __restrict__ grads, int64_t ldg,
-                                          T* __restrict__ min_dist, const Tiling& tl) {
+                                          T* __restrict__ min_dist, const Tiling& tl, unsigned char* smem) {
+    // gradient kernels: the union's KBox records into LDS (see kCollLdsBoxes); the launcher gives
+    // the workgroup min(n_boxes, kCollLdsBoxes) * sizeof(KBox<T>) bytes
+    const bool use_lds = GRAD && a.n_boxes <= kCollLdsBoxes;  // uniform
+    if (use_lds) {
+        const int words = a.n_boxes * (int)(sizeof(KBox<T>) / 16);
+        for (int w = (int)threadIdx.x; w < words; w += (int)blockDim.x)
+            reinterpret_cast<uint4*>(smem)[w] = reinterpret_cast<const uint4*>(boxes)[w];
+        __syncthreads();
+    }
     const uint32_t b = blockIdx.x;
     if ((uint64_t)b * blockDim.x + threadIdx.x >= (uint64_t)n) return;
     // tiled SoA (kin_coll_batch_tiled): this workgroup's tile moves the array bases (wave-uniform)
@@ -227,9 +257,7 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     }
     const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
     coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs,
-                                broad, bnd, ro,
-                                rz, bx, by, off,
-                          dists, ldd, grads, ldg, dmin);
+                                broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds);
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         step_a<T, KINHIP_COLL_FAST_TRIG != 0>(f, S[s], qa[s], ro[s], rz[s]);  // fp32 fast trig: see top
@@ -240,8 +268,7 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
             ro[s][2] = fma(rz[s][0], o1, -(rz[s][1] * o0));
         }
         coll_spheres<T, MAXA, GRAD>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
-                                    offs, broad, bnd, ro, rz, bx, by, off,
-                              dists, ldd, grads, ldg, dmin);
+                                    offs, broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds);
     }
     if (min_dist) {
         if (a.accumulate) dmin = fmin(dmin, ld_soa(min_dist, 0, 0, off));

@@ -454,6 +454,33 @@ def test_ik_dls_work_queue_identical(dev, fetch_tree):
     np.testing.assert_allclose(a[0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
+def test_ik_dls_bench_config_slices_identical(dev, fetch_tree):
+    """Config 4 as the bench runs it (specialised fp32, 65,536 targets, 4 lanes per target: more
+    waves than stay resident, so they run in two rounds): bit-identical to the same targets solved
+    in slices that fit one round of waves (index_base keeps each target's restart draws), and to
+    itself over 70 back-to-back launches."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    N = 1 << 16
+    dt = torch.float32
+    Qr = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=4242,
+                                dtype=dt, device=dev)
+    T = m.plan(arm, out_links=[gl], dtype=dt).run(Qr)[0][0].contiguous()
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt).specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    kw = dict(max_iters=64, restarts=3, seed=0, lanes=4)
+    ref = plan.ik_dls(T, torch.zeros((8, N), dtype=dt, device=dev), **kw)
+    S = 2048
+    for s in range(0, N, S):
+        q, it, err = plan.ik_dls(T[:, s:s + S].contiguous(), torch.zeros((8, S), dtype=dt, device=dev),
+                                 index_base=s, **kw)
+        assert torch.equal(q, ref[0][:, s:s + S]) and torch.equal(it, ref[1][s:s + S]), s
+        assert torch.equal(err, ref[2][:, s:s + S]), s
+    outs = [plan.ik_dls(T, torch.zeros((8, N), dtype=dt, device=dev), **kw) for _ in range(70)]
+    for k, o in enumerate(outs):
+        assert torch.equal(o[0], ref[0]) and torch.equal(o[1], ref[1]) and torch.equal(o[2], ref[2]), k
+    assert float((ref[1] <= 64).float().mean()) >= 0.99
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_ik_dls_acceptance(dev, fetch_tree, dtype):
     """Reachable random targets: converged solutions meet the reference test's criteria

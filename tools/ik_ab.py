@@ -34,7 +34,7 @@ for dt in ((torch.float32,) if os.environ.get("AB_F32") else (torch.float32, tor
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
-    out.append(f"{str(dt)[6:]}: {ms:.3f} ms/batch {n / ms * 1e3:.3e} solves/s succ {(it < 64).float().mean():.4f} "
+    out.append(f"{str(dt)[6:]}: {ms:.3f} ms/batch {n / ms * 1e3:.3e} solves/s succ {(it <= 64).float().mean():.4f} "
                f"mean_it {it.float().mean():.2f} qsum {float(Q.double().sum()):.6f}")
 print(os.path.basename(os.environ.get("KINHIP_LIB", "default")), "G=" + os.environ.get("KINHIP_IK_GROUP", "auto"),
       "Q=" + os.environ.get("KINHIP_IK_QUEUE", "auto"), "spec=" + os.environ.get("AB_SPEC", "0"),

@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
 import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
-BASE = ["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "fk6_64t", "ik32", "ik64", "coll32", "collg32", "coll64"]
+BASE = ["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "fk6_64t", "ik32", "ik64", "coll32", "collg32", "collg32t",
+        "coll64"]
 ap.add_argument("--what", default="fkjac32", choices=BASE + [w + "s" for w in BASE],
                 help="workload; a trailing 's' runs the plan-specialised kernels (kin_plan_specialize)")
 ap.add_argument("--steps", type=int, default=20)
@@ -79,8 +80,13 @@ elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge sce
     if SPEC:
         cp.specialize()
     grads = a.what.startswith("collg")
-    for _ in range(a.steps):
-        cp.run(sdf, Q, dists=grads, grads=grads, min_dist=not grads)
+    if a.what.endswith("t"):  # tiled layout (bench: dists_grads_tiled)
+        Qt = kinhip.tiled(Q, a.tile)
+        for _ in range(a.steps):
+            cp.run_tiled(sdf, Qt, a.n, dists=True, grads=True)
+    else:
+        for _ in range(a.steps):
+            cp.run(sdf, Q, dists=grads, grads=grads, min_dist=not grads)
 else:
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     if SPEC:

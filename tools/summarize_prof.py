@@ -27,6 +27,13 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
                  "FK + 6x8 J, fp32, N = 2^20, plain SoA rows padded by 256, plan-specialised kernel"),
     "fkjac32ts": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
                   "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile 8192), plan-specialised kernel (bench headline)"),
+    "fkjac32ts22": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 22),
+                    "FK + 6x8 J, fp32, N = 2^22 (4x the Infinity Cache), tiled SoA (tile 8192), specialised"),
+    "fkjac32ts24": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 24),
+                    "FK + 6x8 J, fp32, N = 2^24 (16x the Infinity Cache), tiled SoA (tile 8192), specialised"),
+    "collg32ts": ("kinhip_jit_coll_1_f32", (8 + 14 + 14 * 8) * 4 * (1 << 20),
+                  "config 5 / IneqConst: 14 distances + 14x8 gradients, fp32, N = 2^20, tiled SoA (tile 8192), "
+                  "specialised"),
     "fkjac64ts": ("kinhip_jit_fk_f64", (8 + 12 + 48) * 8 * (1 << 20),
                   "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile as run), plan-specialised kernel"),
     "fk6_64ts": ("kinhip_jit_fk_f64", (8 + 72) * 8 * (1 << 20),
@@ -50,19 +57,61 @@ N_CU, N_SIMD = 256, 4
 
 
 def valu_metrics(c):
-    """VALU utilisation from the SQ counters (gfx94x formulas; MI355X_MICROARCH.md: SQ_ACTIVE_INST_*
-    count quad-cycles, GRBM_GUI_ACTIVE is summed over the 8 XCDs)."""
+    """VALU utilisation from the SQ counters (MI355X_MICROARCH.md: SQ_* cycle counters count
+    quad-cycles per wave; GRBM_GUI_ACTIVE is summed over the 8 XCDs).
+
+    valu_busy = issued VALU instructions x 2 cycles (a wave64 fp32 VALU instruction occupies a SIMD
+    for 2 cycles) / (SIMD count x elapsed cycles): the fraction of SIMD cycles spent issuing VALU
+    work.  It cannot exceed 1 while the elapsed-cycle estimate is right; transcendental and fp64
+    instructions take more than 2 cycles, so for them it is a lower bound.
+    The earlier figure, SQ_ACTIVE_INST_VALU x 4 / (SIMDs x cycles), is kept as
+    `sq_active_inst_valu_ratio`: that counter sums, over waves, the cycles during which each wave has
+    a VALU instruction in flight, and the in-flight cycles of co-resident waves on one SIMD overlap,
+    so the ratio is not a utilisation (it reached 1.10 on the collision kernel)."""
     if "GRBM_GUI_ACTIVE" not in c:
         return {}
     cyc = c["GRBM_GUI_ACTIVE"] / 8.0
     out = {"elapsed_cycles": cyc}
-    if "SQ_ACTIVE_INST_VALU" in c:
-        out["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (N_CU * N_SIMD) / cyc
-    if "SQ_INSTS_VALU" in c:  # wave64 fp32 VALU op = 2 cycles on a SIMD (SIMD-32 issue)
-        out["valu_issue_frac_fp32"] = c["SQ_INSTS_VALU"] * 2 / (N_CU * N_SIMD) / cyc
+    if "SQ_INSTS_VALU" in c:
+        out["valu_busy"] = c["SQ_INSTS_VALU"] * 2 / (N_CU * N_SIMD) / cyc
         if "SQ_WAVES" in c:
             out["valu_insts_per_wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+    if "SQ_ACTIVE_INST_VALU" in c:
+        out["sq_active_inst_valu_ratio"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (N_CU * N_SIMD) / cyc
     return out
+
+
+def mem_metrics(c):
+    """Memory-side backpressure and address translation (TCC / TCP counters, when collected):
+    write-credit stall cycles of the L2 -> memory path per elapsed cycle (summed over the 16 TCC
+    channels of each XCD, so a rate of 1 means one channel stalled all the time on average per XCD),
+    and the UTCL1 (per-CU TLB) miss fraction."""
+    out = {}
+    cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8.0
+    for k in ("TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum", "TCC_EA0_WRREQ_STALL_sum"):
+        if k in c:
+            out[k] = c[k]
+            if cyc:
+                out[k.replace("_sum", "_per_cycle")] = c[k] / cyc
+    if "TCP_UTCL1_TRANSLATION_MISS_sum" in c and "TCP_UTCL1_REQUEST_sum" in c:
+        out["utcl1_requests"] = c["TCP_UTCL1_REQUEST_sum"]
+        out["utcl1_misses"] = c["TCP_UTCL1_TRANSLATION_MISS_sum"]
+        out["utcl1_miss_frac"] = c["TCP_UTCL1_TRANSLATION_MISS_sum"] / max(1.0, c["TCP_UTCL1_REQUEST_sum"])
+    return out
+
+
+def recompute(paths):
+    """Rewrite the `valu` block of committed PMC summaries from their stored SQ / GRBM counters."""
+    for p in paths:
+        with open(p) as f:
+            d = json.load(f)
+        if not d.get("sq"):
+            continue
+        d["valu"] = valu_metrics(d["sq"])
+        d["valu_note"] = "valu block recomputed by tools/summarize_prof.py --recompute (issue-based valu_busy)"
+        with open(p, "w") as f:
+            json.dump(d, f, indent=1)
+        print(os.path.basename(p), {k: round(v, 3) for k, v in d["valu"].items() if k != "elapsed_cycles"})
 
 
 def counters(tag):
@@ -85,7 +134,11 @@ def stats(path, kern):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r01")
+    ap.add_argument("--recompute", nargs="*", help="rewrite the valu block of these profiles/*_pmc_*.json files")
     a = ap.parse_args()
+    if a.recompute is not None:
+        recompute(a.recompute or sorted(glob.glob(os.path.join(OUT, "*pmc_*.json"))))
+        return
     os.makedirs(OUT, exist_ok=True)
     for tag, (kern, alg, note) in WORK.items():
         c = counters(tag)
@@ -106,13 +159,16 @@ def main():
              "achieved_GBs_trace": (alg / float(st["AverageNs"])) if st else None,
              "sq": {k: v for k, v in c.items() if k.startswith(("SQ_", "GRBM_"))},
              "valu": valu_metrics(c),
+             "memory_side": mem_metrics(c),
              "method": "rocprofv3 --kernel-trace --stats, then separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ_*), "
                        "20 launches each via tools/prof_kernel.py; hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950)"}
         with open(os.path.join(OUT, f"{a.round}_pmc_{tag}.json"), "w") as f:
             json.dump(d, f, indent=1)
-        if tag == "fkjac32ts":  # the headline kernel's PMC pass, read by bench.py (roofline.traffic)
-            with open(os.path.join(OUT, "pmc_fk_jac_f32.json"), "w") as f:
-                json.dump(d, f, indent=1)
+        # the headline kernel's and the fp64 leg's PMC passes, read by bench.py (roofline.traffic)
+        for t_, fn in (("fkjac32ts", "pmc_fk_jac_f32.json"), ("fkjac64ts", "pmc_fk_jac_f64.json")):
+            if tag == t_:
+                with open(os.path.join(OUT, fn), "w") as f:
+                    json.dump(d, f, indent=1)
         print(json.dumps({k: d[k] for k in ("workload", "hbm_bytes_per_launch", "traffic_over_algorithmic",
                                             "avg_duration_ns_trace", "achieved_GBs_trace")}))
     b = os.path.join(PROF, "bench", "bench_kernel_stats.csv")
