@@ -535,7 +535,9 @@ def main():
                 ach = bytes_per_eval * (1 << lg) / (d_b / k_s) / 1e9
                 big[f"2^{lg}"] = {"evals_per_s": (1 << lg) * ws * k_s / w_b, "avg_launch_us": d_b / k_s * 1e6,
                                   "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
-                                  "working_set_MB": bytes_per_eval * (1 << lg) / 1e6}
+                                  "working_set_MB": bytes_per_eval * (1 << lg) / 1e6,
+                                  "kernel": ("kinhip_jit_fks (grid-strided, 2 configurations per lane)"
+                                             if lg >= 23 and args.spec else "as the headline")}
             out["roofline"]["large_batches"] = big
     if args.extras and headline_spec:
         # the same workload through the most literal form of the API: generic kernel (no run-time

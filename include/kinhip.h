@@ -296,7 +296,14 @@ KINHIP_API int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* des
  * (truncation_dist, src/collision.jl:84-87).  The SDF gradient is analytic
  * (the reference takes a forward difference, eps 1e-7).  fp32 places the
  * spheres with the hardware sin / cos (~4e-7 error; fp64 is exact).  With a
- * finite truncation, spheres provably beyond it skip the boxes (same results). */
+ * finite truncation, spheres provably beyond it skip the boxes (same results).
+ * Gradient columns of joints that do not move a sphere are 0.  (Deliberate
+ * difference: the reference allocates its 3 x n_dof `jac` once outside the
+ * sphere loop, src/collision.jl:76, and get_jacobian! writes only the columns
+ * relevant to each sphere's link, so a sphere that follows one on a deeper
+ * link inherits that sphere's columns; the zeros here are the true
+ * derivative.  Parity for such mixed-link sphere orders is therefore pinned
+ * against the finite-difference truth, not the reference's buffer.) */
 KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq,
                               int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
                               void* stream);

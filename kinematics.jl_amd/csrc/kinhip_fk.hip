@@ -59,10 +59,24 @@ __global__ __launch_bounds__(256) void k_pose_residual(const T* __restrict__ pos
 
 }  // namespace
 
+// batches from this size on run the grid-strided specialised k_fk (launch_fk)
+constexpr int64_t kFkStrideMin = int64_t(1) << 23;
+
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
-                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipFunction_t jit,
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, const JitFns* jf,
                      hipStream_t st) {
+    // Batches whose arrays far exceed the 256 MiB Infinity Cache run the grid-strided specialised
+    // kernel with 2 configurations per lane: the next configuration's angles are in flight while
+    // this one is computed and stored (2^24 fp32 FK + J: 799 -> 733 us; at 2^22 the two are within
+    // 1% (160 / 162 us) and at 2^20 the one-per-lane grid is faster: 41 vs 46 us; tools/fk_stride_ab.py,
+    // profiles/r02_fk_stride_ab.txt).
+    // KINHIP_FK_PER_LANE=<k> forces k configurations per lane (1: the plain kernel).
+    static const int per_lane_env = [] {
+        const char* e = getenv("KINHIP_FK_PER_LANE");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? v : 0;
+    }();
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
@@ -75,12 +89,15 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const T* qc = q ? q + tq : q;
         T* pc = poses ? poses + tp : poses;
         T* jc = jac ? jac + tj : jac;
-        if (jit) {
+        if (jf && jf->fk) {
+            const int per_lane = per_lane_env ? per_lane_env : (n >= kFkStrideMin && jf->fk_stride ? 2 : 1);
+            const hipFunction_t jit = per_lane > 1 && jf->fk_stride ? jf->fk_stride : jf->fk;
+            const unsigned gx = jit == jf->fk ? grid.x : (grid.x + per_lane - 1) / per_lane;
             int64_t cc = c;
             void* args[] = {(void*)&qc, (void*)&ldq, (void*)&cc, (void*)&pc, (void*)&ldp, (void*)&jc, (void*)&ldj,
                             (void*)&tl};
             // (specialised kernels keep branch frames in registers: no dynamic LDS)
-            const hipError_t e = hipModuleLaunchKernel(jit, grid.x, 1, 1, block.x, 1, 1, 0, st, args, nullptr);
+            const hipError_t e = hipModuleLaunchKernel(jit, gx, 1, 1, block.x, 1, 1, 0, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }
@@ -109,7 +126,7 @@ hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, in
 
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_fk<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, \
-                                     int64_t, T*, int64_t, T*, int64_t, const TileArgs&, hipFunction_t,      \
+                                     int64_t, T*, int64_t, T*, int64_t, const TileArgs&, const JitFns*,      \
                                      hipStream_t);                                                           \
     template hipError_t launch_pose_residual<T>(const T*, int64_t, const T*, int64_t, int64_t, int, T*, int64_t, \
                                                 hipStream_t);

@@ -14,10 +14,73 @@ namespace {
 // through the scalar cache) and the plan-specialised kernels compiled at run
 // time (kinhip_jit.cpp: P and S are constexpr, so every step's F, X, kind and
 // column mask fold into the instruction stream).
+// angles (and base pose) of unit b (256 configurations) for this lane
 template <typename T, int MAXA>
+__device__ __forceinline__ void fk_load(const KProg<T>& P, const KStep<T>* __restrict__ S, const T* __restrict__ q,
+                                        int64_t ldq, const Tiling& tl, uint32_t b, T (&qa)[MAXA], T (&bq)[3]) {
+    const uint32_t t = b / tl.tile_blocks;
+    const T* qt = q ? q + (int64_t)t * tl.tsq : q;
+    const uint32_t off = ((b - t * tl.tile_blocks) * blockDim.x + threadIdx.x) * (uint32_t)sizeof(T);
+    bq[0] = bq[1] = bq[2] = T(0);
+    if (P.flags & PF_BASE)
+        for (int k = 0; k < 3; ++k) bq[k] = ld_soa(qt, P.base_col + k, ldq, off);
+    // every phase-A angle load issued up front (independent, coalesced)
+#pragma unroll
+    for (int s = 0; s < MAXA; ++s) {
+        const int32_t c = S[s].qcol;
+        qa[s] = c >= 0 ? ld_soa(qt, c, ldq, off) : T(0);
+    }
+}
+
+template <typename T, int MAXA>
+__device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __restrict__ S, T* slots,
+                                       const T* __restrict__ q, int64_t ldq, T* __restrict__ poses, int64_t ldp,
+                                       T* __restrict__ jac, int64_t ldj, const Tiling& tl, uint32_t b,
+                                       const T (&qa)[MAXA], const T (&bq)[3]);
+
+// STRIDE: grid-strided units with the next unit's angles prefetched (launch_fk picks it for batches
+// far larger than the Infinity Cache; specialised kernels only)
+template <typename T, int MAXA, bool STRIDE = false>
 __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __restrict__ S, T* slots,
                                         const T* __restrict__ q, int64_t ldq, int64_t n, T* __restrict__ poses,
                                         int64_t ldp, T* __restrict__ jac, int64_t ldj, const Tiling& tl) {
+    const uint32_t B = blockDim.x, tid = threadIdx.x;
+    T qa[MAXA], bq[3];
+    if constexpr (STRIDE) {
+    // grid-strided units of B configurations: a lane evaluates several, and the next unit's
+    // angles are loaded before this one is computed and stored (no barrier below: lanes past n
+    // only skip their own work)
+    const uint32_t units = (uint32_t)((n + B - 1) / B);
+    uint32_t b = blockIdx.x;
+    if (b >= units) return;
+    if ((uint64_t)b * B + tid < (uint64_t)n) fk_load<T, MAXA>(P, S, q, ldq, tl, b, qa, bq);
+    for (;;) {
+        const uint32_t bn = b + gridDim.x;
+        T qn[MAXA], bqn[3];
+        const bool more = bn < units;
+        if (more && (uint64_t)bn * B + tid < (uint64_t)n) fk_load<T, MAXA>(P, S, q, ldq, tl, bn, qn, bqn);
+        if ((uint64_t)b * B + tid < (uint64_t)n)
+            fk_one<T, MAXA>(P, S, slots, q, ldq, poses, ldp, jac, ldj, tl, b, qa, bq);
+        if (!more) break;
+        b = bn;
+#pragma unroll
+        for (int s = 0; s < MAXA; ++s) qa[s] = qn[s];
+        bq[0] = bqn[0]; bq[1] = bqn[1]; bq[2] = bqn[2];
+    }
+    } else {
+    const uint32_t b = config_block();
+    if ((uint64_t)b * B + tid >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
+    fk_load<T, MAXA>(P, S, q, ldq, tl, b, qa, bq);
+    fk_one<T, MAXA>(P, S, slots, q, ldq, poses, ldp, jac, ldj, tl, b, qa, bq);
+    }
+}
+
+// one configuration per lane of unit b
+template <typename T, int MAXA>
+__device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __restrict__ S, T* slots,
+                                       const T* __restrict__ q, int64_t ldq, T* __restrict__ poses, int64_t ldp,
+                                       T* __restrict__ jac, int64_t ldj, const Tiling& tl, uint32_t b,
+                                       const T (&qa)[MAXA], const T (&bq)[3]) {
     const int B = blockDim.x, tid = threadIdx.x;
 #ifdef KINHIP_JIT
     // specialised kernels: every slot index is a constant, so branch frames live in registers
@@ -29,8 +92,6 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
 #define KIN_SLOT_STORE(sl, fr) slot_store(slots, (sl), B, tid, (fr))
 #define KIN_SLOT_LOAD(sl, fr) slot_load(slots, (sl), B, tid, (fr))
 #endif
-    const uint32_t b = config_block();
-    if ((uint64_t)b * (uint32_t)B + tid >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
     // tiled SoA: this workgroup's tile (wave-uniform) moves the array bases; lanes keep a 32-bit offset
     const uint32_t t = b / tl.tile_blocks;
     if (q) q += (int64_t)t * tl.tsq;
@@ -42,19 +103,7 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
     sk.off = off;
 
     const bool base = (P.flags & PF_BASE) != 0;
-    T bx = T(0), by = T(0), bth = T(0);
-    if (base) {
-        bx = ld_soa(q, P.base_col, ldq, off);
-        by = ld_soa(q, P.base_col + 1, ldq, off);
-        bth = ld_soa(q, P.base_col + 2, ldq, off);
-    }
-    // every phase-A angle load issued up front (independent, coalesced)
-    T qa[MAXA];
-#pragma unroll
-    for (int s = 0; s < MAXA; ++s) {
-        const int32_t c = S[s].qcol;
-        qa[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
-    }
+    const T bx = bq[0], by = bq[1], bth = bq[2];
     Fr<T> root;
     if (base) base_frame(root, bx, by, bth);
     else set_identity(root);

@@ -989,12 +989,12 @@ int plan_run(const kin_plan* p, const void* q, int64_t ldq, int64_t n, void* pos
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_fk<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, (const float*)q, ldq, n, (float*)poses,
-                             ldp, (float*)jac, ldj, ta, jit_fns(p->jit) ? jit_fns(p->jit)->fk : nullptr,
+                             ldp, (float*)jac, ldj, ta, jit_fns(p->jit),
                              (hipStream_t)stream);
     else
         e = launch_fk<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, (const double*)q, ldq, n,
                               (double*)poses, ldp, (double*)jac, ldj, ta,
-                              jit_fns(p->jit) ? jit_fns(p->jit)->fk : nullptr, (hipStream_t)stream);
+                              jit_fns(p->jit), (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_fk launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }

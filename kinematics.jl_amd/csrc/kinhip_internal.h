@@ -28,15 +28,16 @@ inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0, 0}; }
 // the generic kernel runs.
 struct JitFns {
     hipFunction_t fk = nullptr;
+    hipFunction_t fk_stride = nullptr;  // the same, grid-strided with prefetched angles (launch_fk)
     hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
 };
 
-// jit: the plan-specialised kernel (kinhip_jit.cpp) or null for the generic one
+// jf: the plan-specialised kernels (kinhip_jit.cpp) or null for the generic one
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
-                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, hipFunction_t jit,
+                     int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, const JitFns* jf,
                      hipStream_t st);
 
 struct IkArgs {

@@ -6,7 +6,7 @@
 namespace kinhip {
 template <typename T>
 hipError_t launch_fk(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, int64_t, T*, int64_t,
-                     T*, int64_t, const TileArgs&, hipFunction_t, hipStream_t) {
+                     T*, int64_t, const TileArgs&, const JitFns*, hipStream_t) {
     return hipErrorNoDevice;
 }
 template <typename T>
@@ -31,7 +31,7 @@ hipError_t launch_pose_residual(const T*, int64_t, const T*, int64_t, int64_t, i
 }
 #define KIN_STUBS(T)                                                                                                 \
     template hipError_t launch_fk<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t,        \
-                                     int64_t, T*, int64_t, T*, int64_t, const TileArgs&, hipFunction_t, hipStream_t); \
+                                     int64_t, T*, int64_t, T*, int64_t, const TileArgs&, const JitFns*, hipStream_t); \
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&,        \
                                          const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,            \
                                          const JitFns*, hipStream_t);                                                \

@@ -287,6 +287,27 @@ def test_specialized_fk_equals_generic(dev, fetch_tree, dtype, with_base, rpy_ja
     np.testing.assert_allclose(P1[0].double().cpu().numpy(), ps, atol=TOL[dtype])
 
 
+@pytest.mark.parametrize("with_base", [False, True])
+def test_specialized_strided_large_batch(dev, with_base):
+    """Batches of >= 2^23 configurations run the grid-strided specialised k_fk (two configurations per
+    lane, the next one's angles prefetched; launch_fk): equal to the generic kernel on plain and tiled
+    layouts, with a partial last unit and a partial last tile, and phase-B links in the plan."""
+    m, arm = _fetch(with_base)
+    gl = m.find_link("gripper_link")
+    links = [gl, m.find_link("wrist_flex_link"), m.find_link("head_camera_rgb_optical_frame")]
+    N = (1 << 23) + 1000
+    dt = torch.float32
+    Q = _rand_q(N, 8 + (3 if with_base else 0), 23, dt, dev)
+    gen = m.plan(arm, out_links=links, jac_link=gl, dtype=dt)
+    spe = m.plan(arm, out_links=links, jac_link=gl, dtype=dt).specialize(kinhip.KIN_SPEC_FK)
+    P0, J0 = gen.run(Q)
+    P1, J1 = spe.run(Q)
+    assert torch.equal(P0, P1) and torch.equal(J0, J1)
+    del P1, J1
+    Pt, Jt = spe.run_tiled(kinhip.tiled(Q, 8192), N)
+    assert torch.equal(kinhip.untiled(Pt, N), P0) and torch.equal(kinhip.untiled(Jt, N), J0)
+
+
 def test_specialized_column_semantics(dev, fetch_tree):
     """Specialised plans honour m.angles of non-batched joints, repeated / irrelevant columns and
     get_jacobian! (untouched) vs get_jacobian (zeros) like the generic ones."""

@@ -3,10 +3,12 @@
 //   soa      element (i, r) at r*ld + i            (Julia Matrix(N, rows); ld = N + 256)
 //   tile<T>  element (i, r) at (i/T)*rows*T + r*T + i%T   (Julia Array(T, rows, N/T))
 //   fill     one contiguous write stream of the same bytes (ceiling)
-// Build: hipcc -O3 --offload-arch=gfx950 tools/tile_probe.hip -o gpurun_out/tile_probe
+// Build: hipcc -O3 --offload-arch=gfx950 tools/tile_probe.hip -o kinematics.jl_amd/lib/tile_probe
+// Run:   tile_probe <rows R> [log2 sizes, e.g. 20,22,24]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s\n", hipGetErrorString(e)); return 1; } } while (0)
 
@@ -58,7 +60,13 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (long n : {1L << 20, 1L << 22}) {
+    // sizes: argv[2] = comma-separated log2 sizes (default 20,22)
+    std::vector<long> sizes;
+    for (const char* p = argc > 2 ? argv[2] : "20,22"; *p;) {
+        sizes.push_back(1L << strtol(p, (char**)&p, 10));
+        if (*p == ',') ++p;
+    }
+    for (long n : sizes) {
         const long ldp = n + 8192;
         float *q, *out;
         CK(hipMalloc(&q, 8 * ldp * 4));
