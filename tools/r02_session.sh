@@ -30,6 +30,8 @@ for s in "$@"; do
     bench) step bench 900 python bench.py --steps 50 --warmup 10 ;;
     pytest) step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    dist2) step dist2 600 env KINHIP_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+             --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 5 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
