@@ -44,80 +44,105 @@ __device__ __forceinline__ double signed_sqrt(double k) { return copysign(sqrt(f
 // fp32); larger unions gather from global memory.
 constexpr int kCollLdsBoxes = 64;
 
-template <typename T, bool GRAD>
-__device__ __forceinline__ T union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
-                                       int nb, T px, T py, T pz, T (&gw)[3], const unsigned char* smem,
-                                       bool use_lds) {
-    T best = T(INFINITY);
-    int bk = 0;
+// UnionSDF of NS points at once (NS = 2: two spheres of one link share every box's data, loaded
+// once through the scalar cache, and the loop overhead).  d[i] = sdf(p_i); GRAD: gw[i] = its
+// analytic gradient.
+template <typename T, bool GRAD, int NS>
+__device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
+                                          int nb, const T (&px)[NS], const T (&py)[NS], const T (&pz)[NS],
+                                          T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem, bool use_lds) {
+    T best[NS];
+    int bk[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        best[i] = T(INFINITY);
+        bk[i] = 0;
+    }
     // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
 #pragma clang loop vectorize(disable) unroll_count(KINHIP_AABB_UNROLL)
     for (int k = 0; k < na; ++k) {  // axis-aligned boxes: no rotation
         const KAabb<T>& b = aabb[k];
-        const T key = box_key(fabs(px - b.c[0]) - b.half[0], fabs(py - b.c[1]) - b.half[1],
-                              fabs(pz - b.c[2]) - b.half[2]);
-        if (GRAD) {
-            if (key < best) {
-                best = key;
-                bk = k;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const T key = box_key(fabs(px[i] - b.c[0]) - b.half[0], fabs(py[i] - b.c[1]) - b.half[1],
+                                  fabs(pz[i] - b.c[2]) - b.half[2]);
+            if (GRAD) {
+                if (key < best[i]) {
+                    best[i] = key;
+                    bk[i] = k;
+                }
+            } else {
+                best[i] = fmin(best[i], key);
             }
-        } else {
-            best = fmin(best, key);
         }
     }
 #pragma clang loop vectorize(disable)
     for (int k = na; k < nb; ++k) {
         const KBox<T>& b = boxes[k];
-        const T qx = fabs(fma(b.inv[0], px, fma(b.inv[1], py, fma(b.inv[2], pz, b.inv[3])))) - b.half[0];
-        const T qy = fabs(fma(b.inv[4], px, fma(b.inv[5], py, fma(b.inv[6], pz, b.inv[7])))) - b.half[1];
-        const T qz = fabs(fma(b.inv[8], px, fma(b.inv[9], py, fma(b.inv[10], pz, b.inv[11])))) - b.half[2];
-        const T key = box_key(qx, qy, qz);
-        if (GRAD) {
-            if (key < best) {
-                best = key;
-                bk = k;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const T qx = fabs(fma(b.inv[0], px[i], fma(b.inv[1], py[i], fma(b.inv[2], pz[i], b.inv[3])))) - b.half[0];
+            const T qy = fabs(fma(b.inv[4], px[i], fma(b.inv[5], py[i], fma(b.inv[6], pz[i], b.inv[7])))) - b.half[1];
+            const T qz = fabs(fma(b.inv[8], px[i], fma(b.inv[9], py[i], fma(b.inv[10], pz[i], b.inv[11])))) - b.half[2];
+            const T key = box_key(qx, qy, qz);
+            if (GRAD) {
+                if (key < best[i]) {
+                    best[i] = key;
+                    bk[i] = k;
+                }
+            } else {
+                best[i] = fmin(best[i], key);
             }
-        } else {
-            best = fmin(best, key);
         }
     }
-    const T d = signed_sqrt(best);
-    if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
-        KBox<T> b;
-        if (use_lds) {
-            const KBox<T>* lb = reinterpret_cast<const KBox<T>*>(smem);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) b.inv[i] = lb[bk].inv[i];
+    for (int i = 0; i < NS; ++i) {
+        d[i] = signed_sqrt(best[i]);
+        if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
+            KBox<T> b;
+            if (use_lds) {
+                const KBox<T>* lb = reinterpret_cast<const KBox<T>*>(smem);
 #pragma unroll
-            for (int i = 0; i < 3; ++i) b.half[i] = lb[bk].half[i];
-        } else {
+                for (int j = 0; j < 12; ++j) b.inv[j] = lb[bk[i]].inv[j];
 #pragma unroll
-            for (int i = 0; i < 12; ++i) b.inv[i] = boxes[bk].inv[i];
+                for (int j = 0; j < 3; ++j) b.half[j] = lb[bk[i]].half[j];
+            } else {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) b.half[i] = boxes[bk].half[i];
+                for (int j = 0; j < 12; ++j) b.inv[j] = boxes[bk[i]].inv[j];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) b.half[j] = boxes[bk[i]].half[j];
+            }
+            T l[3], q[3], gl[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                l[j] = fma(b.inv[4 * j], px[i], fma(b.inv[4 * j + 1], py[i], fma(b.inv[4 * j + 2], pz[i], b.inv[4 * j + 3])));
+                q[j] = fabs(l[j]) - b.half[j];
+            }
+            const T mx = fmax(q[0], fmax(q[1], q[2]));
+            if (mx > T(0)) {  // outside: d = |max(q, 0)|
+                const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
+                const T rn = T(1) / sqrt_t(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) gl[j] = (l[j] < T(0) ? -o[j] : o[j]) * rn;
+            } else {  // inside: d = max(q)
+                const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) gl[j] = (j == im) ? (l[j] < T(0) ? T(-1) : T(1)) : T(0);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                gw[i][j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
         }
-        T l[3], q[3], gl[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            l[i] = fma(b.inv[4 * i], px, fma(b.inv[4 * i + 1], py, fma(b.inv[4 * i + 2], pz, b.inv[4 * i + 3])));
-            q[i] = fabs(l[i]) - b.half[i];
-        }
-        const T mx = fmax(q[0], fmax(q[1], q[2]));
-        if (mx > T(0)) {  // outside: d = |max(q, 0)|
-            const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
-            const T rn = T(1) / sqrt_t(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] = (l[i] < T(0) ? -o[i] : o[i]) * rn;
-        } else {  // inside: d = max(q)
-            const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) gl[i] = (i == im) ? (l[i] < T(0) ? T(-1) : T(1)) : T(0);
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) gw[j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
     }
-    return d;
 }
+
+// Two spheres of a link per pass over the boxes (coll_spheres): 1 = in the min-distance kernel only
+// (default), 2 = in both kernels, 0 = never.  The pair costs ~15 VGPRs: the min-distance kernel keeps
+// 8 waves per SIMD and gains ~2% (fewer scalar box loads and waits); the gradient kernel would drop
+// from 5 to 4 waves per SIMD and lose 5-10% (profiles/r02_coll_ab.txt).
+#ifndef KINHIP_COLL_PAIRS
+#define KINHIP_COLL_PAIRS 1
+#endif
 
 template <typename T, int MAXA, bool GRAD>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
@@ -129,34 +154,35 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              T* __restrict__ grads, int64_t ldg, T& dmin,
                                              const unsigned char* smem, bool use_lds) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
-    for (int k = k0; k < k1; ++k) {
-        const KSphere<T>& sp = sph[k];
-        // (fmz: in specialised kernels the sphere's centre is a constant, often with zero components)
-        const T px = fmz(f.r[0], sp.c[0], fmz(f.r[1], sp.c[1], fmz(f.r[2], sp.c[2], f.t[0])));
-        const T py = fmz(f.r[3], sp.c[0], fmz(f.r[4], sp.c[1], fmz(f.r[5], sp.c[2], f.t[1])));
-        const T pz = fmz(f.r[6], sp.c[0], fmz(f.r[7], sp.c[1], fmz(f.r[8], sp.c[2], f.t[2])));
-        T g[3] = {T(0), T(0), T(0)};
-        // Broad phase (finite truncation only): every box lies inside the world-aligned box
-        // (centre bnd[0..2], half extents bnd[3..5]), so a distance to it beyond trunc + r proves
-        // sdf(p) - r > trunc: the reference would report the truncated value with a zero gradient,
-        // and that is written without evaluating the boxes when the whole wave agrees (wave-uniform
-        // skip; the slack covers rounding of the exact path).  Results are identical to evaluating
-        // every box.
-        bool far = false;
-        if (broad) {
-            const T ox = fmax(fabs(px - bnd[0]) - bnd[3], T(0));
-            const T oy = fmax(fabs(py - bnd[1]) - bnd[4], T(0));
-            const T oz = fmax(fabs(pz - bnd[2]) - bnd[5], T(0));
-            const T lim = fma(trunc + sp.r, T(1.0001), T(1e-5));
-            far = lim > T(0) && fma(ox, ox, fma(oy, oy, oz * oz)) > lim * lim;
-        }
+    // sphere centre in the world (fmz: in specialised kernels the centre is a constant, often with
+    // zero components)
+    auto centre = [&](const KSphere<T>& sp, T& px, T& py, T& pz) {
+        px = fmz(f.r[0], sp.c[0], fmz(f.r[1], sp.c[1], fmz(f.r[2], sp.c[2], f.t[0])));
+        py = fmz(f.r[3], sp.c[0], fmz(f.r[4], sp.c[1], fmz(f.r[5], sp.c[2], f.t[1])));
+        pz = fmz(f.r[6], sp.c[0], fmz(f.r[7], sp.c[1], fmz(f.r[8], sp.c[2], f.t[2])));
+    };
+    // Broad phase (finite truncation only): every box lies inside the world-aligned box (centre
+    // bnd[0..2], half extents bnd[3..5]), so a distance to it beyond trunc + r proves sdf(p) - r >
+    // trunc: the reference would report the truncated value with a zero gradient, and that is
+    // written without evaluating the boxes when the whole wave agrees (wave-uniform skip; the slack
+    // covers rounding of the exact path).  Results are identical to evaluating every box.
+    auto all_far = [&](const KSphere<T>& sp, T px, T py, T pz) -> bool {
+        if (!broad) return false;
+        const T ox = fmax(fabs(px - bnd[0]) - bnd[3], T(0));
+        const T oy = fmax(fabs(py - bnd[1]) - bnd[4], T(0));
+        const T oz = fmax(fabs(pz - bnd[2]) - bnd[5], T(0));
+        const T lim = fma(trunc + sp.r, T(1.0001), T(1e-5));
+        return __all(lim > T(0) && fma(ox, ox, fma(oy, oy, oz * oz)) > lim * lim);
+    };
+    // truncation, margin, outputs and gradient columns of one sphere (sdf value ds, gradient g)
+    auto finish = [&](const KSphere<T>& sp, T px, T py, T pz, bool skipped, T ds, const T (&g)[3]) {
         T d;
         bool cut;
-        if (broad && __all(far)) {
+        if (skipped) {
             d = trunc;
             cut = true;
         } else {
-            d = union_sdf<T, GRAD>(boxes, aabb, na, nb, px, py, pz, g, smem, use_lds) - sp.r;
+            d = ds - sp.r;
             cut = d > trunc;  // truncation_dist (src/collision.jl:84-87)
             if (cut) d = trunc;
         }
@@ -200,6 +226,27 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                 st_soa(grads, b0 + 2, ldg, off, cut ? T(0) : fma(-g[0], py - by, g[1] * (px - bx)));
             }
         }
+    };
+    int k = k0;
+    constexpr bool pairs = KINHIP_COLL_PAIRS == 2 || (KINHIP_COLL_PAIRS == 1 && !GRAD);
+    if constexpr (pairs)
+    for (; k + 1 < k1; k += 2) {  // two spheres of this link per pass over the boxes
+        T px[2], py[2], pz[2], ds[2] = {T(0), T(0)}, g[2][3] = {{T(0), T(0), T(0)}, {T(0), T(0), T(0)}};
+        centre(sph[k], px[0], py[0], pz[0]);
+        centre(sph[k + 1], px[1], py[1], pz[1]);
+        // skip only when both spheres are beyond the truncation wave-wide (the exact path gives the
+        // same results for one that is)
+        const bool far = all_far(sph[k], px[0], py[0], pz[0]) && all_far(sph[k + 1], px[1], py[1], pz[1]);
+        if (!far) union_sdf<T, GRAD, 2>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
+        finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
+        finish(sph[k + 1], px[1], py[1], pz[1], far, ds[1], g[1]);
+    }
+    for (; k < k1; ++k) {
+        T px[1], py[1], pz[1], ds[1] = {T(0)}, g[1][3] = {{T(0), T(0), T(0)}};
+        centre(sph[k], px[0], py[0], pz[0]);
+        const bool far = all_far(sph[k], px[0], py[0], pz[0]);
+        if (!far) union_sdf<T, GRAD, 1>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
+        finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
     }
 }
 
