@@ -379,6 +379,19 @@ def _copy_bw(dev, nbytes=1 << 31):
     return gbs
 
 
+def _pmc_valu(fname):
+    """Issue-based VALU busy of a committed PMC summary (tools/summarize_prof.py), for the legs whose
+    bound is VALU / latency rather than HBM (configs 4 and 5)."""
+    p = os.path.join(ROOT, "profiles", fname)
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    v = d.get("valu", {})
+    return {"valu_busy": v.get("valu_busy"), "valu_insts_per_wave": v.get("valu_insts_per_wave"),
+            "traffic_over_algorithmic": d.get("traffic_over_algorithmic"), "source": "profiles/" + fname}
+
+
 def _pmc_traffic(workload, fname="pmc_fk_jac_f32.json"):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/), if present."""
     p = os.path.join(ROOT, "profiles", fname)
@@ -539,6 +552,9 @@ def main():
                                   "kernel": ("kinhip_jit_fks (grid-strided, 2 configurations per lane)"
                                              if lg >= 23 and args.spec else "as the headline")}
             out["roofline"]["large_batches"] = big
+            out["roofline"]["rocprof_note"] = ("the cold-cache and 2^22 legs launch the headline kernel too (same name); "
+                                               "tools/trace_headline.py splits a rocprofv3 kernel trace of this bench "
+                                               "per leg (profiles/r02_bench_trace_legs.json: the 50 timed launches)")
     if args.extras and headline_spec:
         # the same workload through the most literal form of the API: generic kernel (no run-time
         # compilation), plain column-major rows (padded ld) -- kin_plan_run as a Julia caller would
@@ -598,9 +614,13 @@ def main():
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": lay64}
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec)
+        out["config4_ik_dls"]["pmc"] = _pmc_valu("r02_pmc_ik32s.json")
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
         out["config4_ik_dls_f64"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, dt=torch.float64)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec)
+        out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("r02_pmc_coll32s.json")
+        out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("r02_pmc_collg32s.json")
+        out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("r02_pmc_collg32ts.json")
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
         if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)
             out["generic_kernels"] = {
