@@ -222,6 +222,38 @@ def test_gpu_collision_box_kinds(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_boxes", [64, 65])
+def test_gpu_collision_lds_box_limit(n_boxes):
+    """The gradient kernels gather the argmin box from an LDS copy of the union for up to 64 boxes and
+    from global memory beyond: both sides of the limit, specialised fp32 == generic fp32 (bit-equal)
+    and both vs the oracle."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    rng = np.random.default_rng(100 + n_boxes)
+    poses, widths = [], []
+    for _ in range(n_boxes):
+        R = O.rpy_to_matrix(rng.uniform(-np.pi, np.pi, 3)) if rng.random() < 0.5 else np.eye(3)
+        poses.append(_T(rng.uniform([-1, -1, 0], [1.5, 1, 1.5]), R))
+        widths.append(rng.uniform(0.02, 0.2, 3))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(P, w) for P, w in zip(poses, widths)])
+    N = 2000
+    Q = torch.tensor(rng.uniform(-1.2, 1.2, (8, N)), dtype=torch.float32, device=dev)
+    gen = sscc.plan(arm, dtype=torch.float32)
+    spe = sscc.plan(arm, dtype=torch.float32).specialize()
+    D0, G0, M0 = gen.run(sdf, Q, grads=True, min_dist=True)
+    D1, G1, M1 = spe.run(sdf, Q, grads=True, min_dist=True)
+    assert torch.equal(D0, D1) and torch.equal(G0, G1) and torch.equal(M0, M1)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    box = O.OracleUnionSDF(poses, widths)
+    ids = [tree.joint_id(n) for n in ARM]
+    rd, rg = O.coll_batch(om, box, Q.double().cpu().numpy(), ids, sph, rad)
+    np.testing.assert_allclose(D1.double().cpu().numpy(), rd, atol=2e-5)
+    _assert_mismatches_at_kinks(om, box, Q.double().cpu().numpy(), ids, sph, rad, G1.double().cpu().numpy(), rg,
+                                1e-4, h=1e-5)
+
+
+@pytest.mark.gpu
 def test_gpu_collision_edges_and_errors():
     """Empty / single / ragged batches, a scene of many random boxes, and the error paths."""
     import kinhip
