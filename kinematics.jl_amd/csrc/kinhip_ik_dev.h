@@ -146,15 +146,16 @@ __device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S,
     for (int s = 0; s < MAXA; ++s) {
         const KStep<T>& st = S[s];
         const int32_t c = st.qcol;
-        T v = c >= 0 ? KIN_IK_LD(q, c, ldq, off) : T(0);
-        if (att > 0 && c >= 0) {
-            if (st.flags & SF_REC) {
-                double lo = (double)st.lo, hi = (double)st.hi;
-                if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
-                v = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, c));
-            } else {
-                v = fmin(fmax(v, st.lo), st.hi);  // attempt 0's first step has clamped it
-            }
+        T v;
+        if (att > 0 && c >= 0 && (st.flags & SF_REC)) {
+            // a restart draws the column: no load of q0 (a load here would wait, through
+            // s_waitcnt vmcnt, for every store the wave still has in flight)
+            double lo = (double)st.lo, hi = (double)st.hi;
+            if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
+            v = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, c));
+        } else {
+            v = c >= 0 ? KIN_IK_LD(q, c, ldq, off) : T(0);
+            if (att > 0 && c >= 0) v = fmin(fmax(v, st.lo), st.hi);  // attempt 0's first step has clamped it
         }
         qs[s] = v;
     }
