@@ -1,0 +1,123 @@
+"""The Julia ccall shim (kinematics.jl_amd/julia/KinematicsHIP.jl) against the C-ABI it binds
+(include/kinhip.h), checked without Julia (not in this image): every `ccall` names an exported
+function with the same number of arguments and the same C type class per argument, and every
+Julia struct that mirrors a C descriptor has the C struct's fields, in order, with matching types
+(so the field offsets Julia lays out are the C ones)."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kinhip.h")
+SHIM = os.path.join(ROOT, "kinematics.jl_amd", "julia", "KinematicsHIP.jl")
+
+STRUCTS = {"KinTreeDesc": "kin_tree_desc", "KinPlanDesc": "kin_plan_desc", "KinIkParams": "kin_ik_params",
+           "KinCollDesc": "kin_coll_desc"}
+
+
+def _strip_c_comments(s):
+    return re.sub(r"/\*.*?\*/", "", re.sub(r"//[^\n]*", "", s, flags=re.S), flags=re.S)
+
+
+def c_class(t):
+    """Type class of a C parameter / field declaration (name stripped)."""
+    t = t.strip()
+    if "*" in t:
+        return "ptr"
+    t = re.sub(r"\bconst\b", "", t).split()
+    base = " ".join(t[:-1]) if len(t) > 1 else t[0]
+    return {"int32_t": "i32", "int": "i32", "uint32_t": "u32", "int64_t": "i64", "uint64_t": "u64",
+            "double": "f64", "float": "f32", "size_t": "u64"}[base]
+
+
+def jl_class(t):
+    t = t.strip()
+    if t.startswith(("Ptr{", "Ref{")) or t in ("Cstring", "Ptr"):
+        return "ptr"
+    return {"Int32": "i32", "Cint": "i32", "UInt32": "u32", "Int64": "i64", "UInt64": "u64", "Float64": "f64",
+            "Float32": "f32", "Csize_t": "u64", "Cdouble": "f64"}[t]
+
+
+def split_top(s):
+    """Split at commas outside braces / parentheses."""
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "{(":
+            depth += 1
+        elif ch in "})":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur)
+    return [x.strip() for x in out if x.strip()]
+
+
+def c_functions():
+    src = _strip_c_comments(open(HEADER).read())
+    funcs = {}
+    for m in re.finditer(r"KINHIP_API\s+([\w\s\*]+?)\s*\b(\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.S):
+        ret, name, params = m.group(1), m.group(2), m.group(3)
+        ps = [] if params.strip() in ("", "void") else [re.sub(r"\s*\b\w+\s*$", "", p) if not p.strip().endswith("*")
+                                                        else p for p in split_top(params)]
+        funcs[name] = (c_class(ret + " x"), [c_class(p + " x") for p in ps])
+    return funcs
+
+
+def jl_ccalls():
+    src = open(SHIM).read()
+    calls = []
+    for m in re.finditer(r"ccall\(\(:(\w+),\s*libkinhip\),\s*", src):
+        i = m.end()
+        depth, j = 0, i  # return type: up to the next top-level comma
+        while not (src[j] == "," and depth == 0):
+            depth += src[j] in "{(" and 1 or (-1 if src[j] in "})" else 0)
+            j += 1
+        ret = src[i:j].strip()
+        k = src.index("(", j)  # the argument-type tuple
+        depth, e = 0, k
+        while True:
+            depth += 1 if src[e] == "(" else (-1 if src[e] == ")" else 0)
+            if depth == 0:
+                break
+            e += 1
+        calls.append((m.group(1), ret, split_top(src[k + 1:e])))
+    return calls
+
+
+def test_every_ccall_matches_a_c_prototype():
+    funcs = c_functions()
+    calls = jl_ccalls()
+    assert len(calls) >= 15
+    for name, ret, args in calls:
+        assert name in funcs, f"{name}: not exported by include/kinhip.h"
+        cret, cargs = funcs[name]
+        assert jl_class(ret) == cret, (name, ret, cret)
+        assert len(args) == len(cargs), (name, args, cargs)
+        for a, c in zip(args, cargs):
+            assert jl_class(a) == c, (name, a, c)
+
+
+@pytest.mark.parametrize("jl_name", sorted(STRUCTS))
+def test_julia_struct_mirrors_c_struct(jl_name):
+    jl = open(SHIM).read()
+    m = re.search(r"^struct %s\n(.*?)^end" % jl_name, jl, flags=re.S | re.M)
+    assert m, jl_name
+    jf = [tuple(x.strip().split("::")) for x in m.group(1).strip().splitlines() if "::" in x]
+    c = _strip_c_comments(open(HEADER).read())
+    cm = re.search(r"typedef struct %s \{(.*?)\}\s*%s;" % (STRUCTS[jl_name], STRUCTS[jl_name]), c, flags=re.S)
+    assert cm, STRUCTS[jl_name]
+    cf = []
+    for decl in cm.group(1).split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        name = re.search(r"(\w+)\s*$", decl).group(1)
+        cf.append((name, c_class(decl)))
+    assert [n for n, _ in jf] == [n for n, _ in cf], (jl_name, jf, cf)
+    for (n, t), (_, cc) in zip(jf, cf):
+        assert jl_class(t) == cc, (jl_name, n, t, cc)
