@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -196,7 +197,16 @@ struct kin_plan {
     int32_t n_steps = 0;
     JitKernels* jit = nullptr;
     uint32_t jit_mask = 0;
+    // two-phase IK schedule scratch (launch_ik_dls): allocated at the first kin_ik_dls_batch call;
+    // kIkScratchSets sets used in turn, so launches of one plan on several streams at once do not
+    // share a list (up to kIkScratchSets in flight)
+    static constexpr int kIkScratchSets = 4;
+    static constexpr int64_t kIkScratchCap = int64_t(1) << 20;
+    mutable std::mutex ik_mu;
+    mutable void* d_ikscr = nullptr;
+    mutable std::atomic<uint32_t> ik_seq{0};
     ~kin_plan() {
+        if (d_ikscr) (void)hipFree(d_ikscr);
         jit_destroy(jit);
         if (d_steps) (void)hipFree(d_steps);
         if (d_sph) (void)hipFree(d_sph);
@@ -1382,13 +1392,32 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     const bool narrow = (12 * ldt + span) * esz < (int64_t(1) << 31) && (p->nqcols * ldq + span) * esz < (int64_t(1) << 31) &&
                         (2 * lde + span) * esz < (int64_t(1) << 31);
     const JitFns* jf = narrow ? jit_fns(p->jit) : nullptr;
+    // two-phase schedule scratch (small batches with restarts; launch_ik_dls)
+    IkScratch scr;
+    if (prm->restarts > 0 && n <= kin_plan::kIkScratchCap) {
+        const size_t set_bytes = sizeof(int32_t) * kin_plan::kIkScratchCap + 256;
+        {
+            std::lock_guard<std::mutex> lk(p->ik_mu);
+            if (!p->d_ikscr) {
+                hipError_t e0 = hipMalloc(&p->d_ikscr, set_bytes * kin_plan::kIkScratchSets);
+                if (e0 != hipSuccess) {
+                    p->d_ikscr = nullptr;
+                    return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e0));
+                }
+            }
+        }
+        unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * (p->ik_seq.fetch_add(1) % kin_plan::kIkScratchSets);
+        scr.fail_n = (uint32_t*)base;
+        scr.fail_list = (int32_t*)(base + 256);
+        scr.cap = kin_plan::kIkScratchCap;
+    }
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,
-                                 (float*)q, ldq, n, iters, (float*)err, lde, jf, (hipStream_t)stream);
+                                 (float*)q, ldq, n, iters, (float*)err, lde, jf, scr, (hipStream_t)stream);
     else
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
-                                  (double*)q, ldq, n, iters, (double*)err, lde, jf, (hipStream_t)stream);
+                                  (double*)q, ldq, n, iters, (double*)err, lde, jf, scr, (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }

@@ -46,11 +46,11 @@ static int ik_group(int64_t n, int n_attempts, int lanes) {
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, const JitFns* jf, hipStream_t st) {
+                         int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st) {
     const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
     const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
-                  0};
+                  0, 0, 0, nullptr, nullptr, nullptr};
     const int G = ik_group(n, natt, a.lanes);
     static const int cus = [] {
         int dev = 0, c = 0;
@@ -65,44 +65,44 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         return e ? atoi(e) : 0;
     }();
     const int64_t resident_waves = (int64_t)cus * (res_env > 0 ? res_env : 8);
-    const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
-    for (int64_t s0 = 0; s0 < n; s0 += chunk) {
-        at.ibase = a.index_base + s0;
-        const int64_t c = std::min(chunk, n - s0);
-        const int64_t ng = 64 / G;
-        // queue depth: one target per group (no refill) while the batch fills the chip in at most
-        // two rounds of waves, else as many waves as stay resident, each working through its share
-        static const int qmode = [] {
-            const char* e = getenv("KINHIP_IK_QUEUE");
-            return e ? atoi(e) : -1;
-        }();
-        const int64_t plain = (c + ng - 1) / ng;
-        const bool queue = qmode >= 0 ? qmode != 0 : plain > 2 * resident_waves;
-        const int64_t waves = queue ? std::min(resident_waves, plain) : plain;
-        const int64_t per_wave = (c + waves - 1) / waves;  // targets each wave works through
-        const int64_t nw = (c + per_wave - 1) / per_wave;
+    // queue depth: one target per group (no refill) while the batch fills the chip in at most
+    // two rounds of waves, else as many waves as stay resident, each working through its share
+    static const int qmode = [] {
+        const char* e = getenv("KINHIP_IK_QUEUE");
+        return e ? atoi(e) : -1;
+    }();
+    // Two-phase schedule (KINHIP_IK_TWO_PHASE=<0|1>, default: automatic): small batches fill the
+    // chip only by running the restart attempts of a target side by side (G lanes), and a wave then
+    // lasts as long as any of its targets' attempts.  Phase 1 runs attempt 0 of every target on one
+    // lane and writes the solved ones; phase 2 runs attempts 1, 2, ... side by side for the ones
+    // attempt 0 did not solve, packed densely (fail_list).  Each attempt's arithmetic is unchanged
+    // and the lowest converged attempt is still the one written: results are identical.
+    static const int tp_env = [] {
+        const char* e = getenv("KINHIP_IK_TWO_PHASE");
+        return e ? atoi(e) : -1;
+    }();
+    auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw) -> hipError_t {
         const dim3 grid((unsigned)((nw * 64 + 255) / 256)), block(256);
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
-        const hipFunction_t jk = jf ? jf->ik[a.with_rot ? 1 : 0][G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : 3] : nullptr;
+        const hipFunction_t jk =
+            jf ? jf->ik[a.with_rot ? 1 : 0][GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3] : nullptr;
         if (jk) {
             int64_t cc = c, pw = per_wave;
-            void* args[] = {(void*)&at, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
+            void* args[] = {(void*)&ar, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
                             (void*)&ic, (void*)&ec, (void*)&lde, (void*)&pw};
-            const hipError_t e = hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
-            if (e != hipSuccess) return e;
-            continue;
+            return hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
         }
-#define KIN_IK_G(MA, R, GG) \
-        hipLaunchKernelGGL((k_ik_dls<T, MA, R, GG>), grid, block, 0, st, P, steps, at, tc, ldt, qc, ldq, c, ic, ec, lde, per_wave)
+#define KIN_IK_G(MA, R, GX) \
+        hipLaunchKernelGGL((k_ik_dls<T, MA, R, GX>), grid, block, 0, st, P, steps, ar, tc, ldt, qc, ldq, c, ic, ec, lde, per_wave)
 #define KIN_IK6(MA) \
-        switch (G) { case 2: KIN_IK_G(MA, 6, 2); break; case 4: KIN_IK_G(MA, 6, 4); break; \
-                     case 8: KIN_IK_G(MA, 6, 8); break; default: KIN_IK_G(MA, 6, 1); }
+        switch (GG) { case 2: KIN_IK_G(MA, 6, 2); break; case 4: KIN_IK_G(MA, 6, 4); break; \
+                      case 8: KIN_IK_G(MA, 6, 8); break; default: KIN_IK_G(MA, 6, 1); }
 #define KIN_IK3(MA) \
-        switch (G) { case 2: KIN_IK_G(MA, 3, 2); break; case 4: KIN_IK_G(MA, 3, 4); break; \
-                     case 8: KIN_IK_G(MA, 3, 8); break; default: KIN_IK_G(MA, 3, 1); }
+        switch (GG) { case 2: KIN_IK_G(MA, 3, 2); break; case 4: KIN_IK_G(MA, 3, 4); break; \
+                      case 8: KIN_IK_G(MA, 3, 8); break; default: KIN_IK_G(MA, 3, 1); }
         if (a.with_rot) {
             KIN_MAXA_DISPATCH(g.maxA, KIN_IK6)
         } else {
@@ -111,7 +111,41 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
 #undef KIN_IK6
 #undef KIN_IK3
 #undef KIN_IK_G
-        const hipError_t e = hipGetLastError();
+        return hipGetLastError();
+    };
+    const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
+    for (int64_t s0 = 0; s0 < n; s0 += chunk) {
+        at.ibase = a.index_base + s0;
+        const int64_t c = std::min(chunk, n - s0);
+        const int64_t ng = 64 / G;
+        const int64_t plain = (c + ng - 1) / ng;
+        // (automatic: batches that need more than one round of resident waves at G lanes per target
+        // and fit the scratch list; phase 2 runs the remaining attempts side by side)
+        const bool two = scr.fail_list && natt > 1 && c <= scr.cap && a.lanes == 0 &&
+                         (tp_env >= 0 ? tp_env != 0 : plain > resident_waves);
+        if (two) {
+            hipError_t e = hipMemsetAsync(scr.fail_n, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) return e;
+            IkArgsT<T> a1 = at;  // phase 1: attempt 0, one lane per target
+            a1.n_attempts = 1;
+            a1.phase1 = 1;
+            a1.fail_list = scr.fail_list;
+            a1.fail_n = scr.fail_n;
+            if ((e = one(a1, 1, s0, c, 64, (c + 63) / 64)) != hipSuccess) return e;
+            IkArgsT<T> a2 = at;  // phase 2: attempts 1.. of the listed targets, side by side
+            a2.att0 = 1;
+            a2.idx = scr.fail_list;
+            a2.fail_n = scr.fail_n;
+            const int G2 = natt - 1 <= 1 ? 1 : natt - 1 <= 2 ? 2 : natt - 1 <= 4 ? 4 : 8;
+            const int64_t ng2 = 64 / G2;
+            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) return e;
+            continue;
+        }
+        const bool queue = qmode >= 0 ? qmode != 0 : plain > 2 * resident_waves;
+        const int64_t waves = queue ? std::min(resident_waves, plain) : plain;
+        const int64_t per_wave = (c + waves - 1) / waves;  // targets each wave works through
+        const int64_t nw = (c + per_wave - 1) / per_wave;
+        const hipError_t e = one(at, G, s0, c, per_wave, nw);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -144,7 +178,7 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, \
                                          const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,     \
-                                         const JitFns*, hipStream_t);                                         \
+                                         const JitFns*, const IkScratch&, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
                                            int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)

@@ -113,6 +113,15 @@ struct IkArgsT {
     int32_t n_attempts;   // 1 + (max_iters - 1) / attempt_len (attempts the sequential schedule reaches)
     uint64_t seed;
     int64_t ibase;  // global index of this chunk's first configuration
+    // Two-phase schedule (launch_ik_dls, small batches): phase 1 runs attempt 0 of every target
+    // (one lane each) and appends the targets it does not solve to fail_list instead of writing
+    // them; phase 2 runs attempts att0 = 1, 2, ... of the listed targets only (idx = fail_list,
+    // *fail_n of them).  Otherwise att0 = 0, phase1 = 0, idx = null.
+    int32_t att0;
+    int32_t phase1;
+    const int32_t* idx;
+    int32_t* fail_list;
+    uint32_t* fail_n;
 };
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
@@ -174,7 +183,8 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const int lane = (int)(threadIdx.x & 63u);
     const int slot = lane % G, grp = lane / G;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t wbeg = wave * chunk, wend = wbeg + chunk < n ? wbeg + chunk : n;
+    const int64_t nt = a.idx ? (int64_t)*a.fail_n : n;  // phase 2: the listed targets only
+    const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
     int64_t i = 0;
     bool have = false;    // the first pass of the loop hands every group its first target
@@ -199,7 +209,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         if (base)
             for (int k = 0; k < 3; ++k) b0[k] = KIN_IK_LD(q, P.base_col + k, ldq, off);
         b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
-        att = slot;
+        att = a.att0 + slot;
         done = att >= a.n_attempts;
         res_att = INT_MAX;
         final_lane = false;
@@ -220,7 +230,9 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         const bool gfin = have && (dmask & gmask) == gmask;
         if (gfin) {
             const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
-            if (writer) {
+            if (a.phase1 && res_att == INT_MAX) {  // attempt 0 failed: phase 2 takes the target
+                a.fail_list[atomicAdd(a.fail_n, 1u)] = (int32_t)i;
+            } else if (writer) {
 #pragma unroll
                 for (int s2 = 0; s2 < MAXA; ++s2) {
                     const int32_t c = S[s2].qcol;
@@ -241,7 +253,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             const uint64_t lead = 1ull << (grp * G);
             const int rank = __popcll(need & (lead - 1ull));
             if (!have && (need & lead) && next + rank < wend) {
-                i = next + rank;
+                i = a.idx ? (int64_t)a.idx[next + rank] : next + rank;
                 have = true;
                 start_target();  // the single (inlined) initialisation site
             }

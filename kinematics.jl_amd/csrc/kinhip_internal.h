@@ -50,10 +50,18 @@ struct IkArgs {
     int64_t index_base;  // global index of target 0 (restart draws)
 };
 
+// Device scratch of the two-phase IK schedule (launch_ik_dls): the list of targets attempt 0 did
+// not solve and its length, for batches of up to `cap` targets (null: single phase only)
+struct IkScratch {
+    int32_t* fail_list = nullptr;
+    uint32_t* fail_n = nullptr;
+    int64_t cap = 0;
+};
+
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, const JitFns* jf, hipStream_t st);
+                         int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st);
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,

@@ -453,6 +453,34 @@ def test_ik_dls_lanes_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0].cpu().numpy(), rq, atol=1e-7)
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
+    """The two-phase schedule (automatic for this batch: 65,536 targets, 6 attempts of 4 iterations)
+    returns the single-phase schedules' angles, iteration counts and errors bit for bit (lanes=1:
+    sequential attempts, lanes=4: side by side), and fp64 matches the oracle on a subset."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 1 << 16
+    tgt = _targets(om, ids, gl.id, N, 57)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    if dtype == torch.float32:
+        plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
+    kw = dict(max_iters=23, restarts=4, seed=5, lam=1e-2, max_step=0.5)
+    res = [plan.ik_dls(T, torch.zeros((8, N), dtype=dtype, device=dev), lanes=lanes, **kw) for lanes in (0, 1, 4)]
+    it0 = res[0][1].cpu().numpy()
+    assert len(set((it0 // 4).tolist())) > 3  # winners spread over several attempts: phase 2 does work
+    for Q, it, err in res[1:]:
+        assert torch.equal(Q, res[0][0]) and torch.equal(it, res[0][1]) and torch.equal(err, res[0][2])
+    if dtype == torch.float64:
+        k = 1000
+        rq, rit, _ = om.ik_dls_batch(np.zeros((8, k)), ids, gl.id, tgt[:, :k], **kw)
+        np.testing.assert_array_equal(it0[:k], rit)
+        np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
+
+
 def test_ik_dls_work_queue_identical(dev, fetch_tree):
     """Large batches run as per-wave work queues (a lane group that finishes takes the wave's next
     target): bit-identical to one target per group (lanes=1 here never queues), and the first
@@ -476,10 +504,11 @@ def test_ik_dls_work_queue_identical(dev, fetch_tree):
 
 
 def test_ik_dls_bench_config_slices_identical(dev, fetch_tree):
-    """Config 4 as the bench runs it (specialised fp32, 65,536 targets, 4 lanes per target: more
-    waves than stay resident, so they run in two rounds): bit-identical to the same targets solved
-    in slices that fit one round of waves (index_base keeps each target's restart draws), and to
-    itself over 70 back-to-back launches."""
+    """Config 4 as the bench runs it (specialised fp32, 65,536 targets, automatic schedule = the
+    two-phase one: attempt 0 of every target, then the remaining attempts of the unsolved ones side
+    by side): bit-identical to the same targets solved in slices of 2,048 (one phase, 4 lanes per
+    target; index_base keeps each target's restart draws), and to itself over 70 back-to-back
+    launches (the scratch list sets cycle)."""
     m, arm = _fetch()
     gl = m.find_link("gripper_link")
     N = 1 << 16
@@ -488,7 +517,7 @@ def test_ik_dls_bench_config_slices_identical(dev, fetch_tree):
                                 dtype=dt, device=dev)
     T = m.plan(arm, out_links=[gl], dtype=dt).run(Qr)[0][0].contiguous()
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt).specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
-    kw = dict(max_iters=64, restarts=3, seed=0, lanes=4)
+    kw = dict(max_iters=64, restarts=3, seed=0)
     ref = plan.ik_dls(T, torch.zeros((8, N), dtype=dt, device=dev), **kw)
     S = 2048
     for s in range(0, N, S):
