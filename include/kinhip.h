@@ -25,7 +25,10 @@
  *    of one call.  Host-side tree data is always double.
  *  - Every batched call is asynchronous on the given hipStream_t (passed as
  *    void*; NULL = the null stream) and capture-safe (no allocation, copy or
- *    synchronisation inside).
+ *    synchronisation inside), with one exception: the first kin_ik_dls_batch
+ *    call of a plan that may use the two-phase schedule (restarts > 0, lanes = 0,
+ *    <= 2^20 targets) allocates that plan's scratch (synchronising; make it once
+ *    outside a stream capture).
  *  - Errors: a negative kin_status; kin_last_error() returns a thread-local
  *    message.  Reference exceptions map to: KeyError -> KIN_E_KEY,
  *    MethodError (Jacobian column of a fixed joint) -> KIN_E_METHOD,
@@ -249,7 +252,12 @@ typedef struct kin_ik_params {
     uint64_t seed;
     int32_t lanes;      /* lanes per target running attempts side by side: 0 = auto, else 1/2/4/8.
                            Results are identical for every value (each attempt's arithmetic is the
-                           sequential schedule's); only the parallelism changes. */
+                           sequential schedule's); only the parallelism changes.  With 0 and restarts,
+                           batches of more than one round of waves (up to 2^20 targets) run in two
+                           launches: attempt 0 of every target, then the remaining attempts of the
+                           targets attempt 0 did not solve, side by side (same results).  The two-phase
+                           scratch (first call: hipMalloc, synchronising) is per plan, with 4 sets used in
+                           turn: at most 4 such calls of one plan may be in flight at once. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */

@@ -333,7 +333,9 @@ class Plan:
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
                max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None):
         """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
-        target running restart attempts side by side (0 auto; results identical for every value).
+        target running restart attempts side by side (0 auto, which runs batches of more than one round
+        of waves in two phases: attempt 0 of every target, then the other attempts of the unsolved ones;
+        results identical for every value).
         `index_base`: global index of target 0 for the restart draws (a shard's offset), so a target
         set sharded over ranks solves exactly as in one process.  iters > max_iters: not converged."""
         N = self._check_q(Q)
