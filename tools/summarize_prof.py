@@ -38,8 +38,10 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
                   "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile as run), plan-specialised kernel"),
     "fk6_64ts": ("kinhip_jit_fk_f64", (8 + 72) * 8 * (1 << 20),
                  "FK of 6 links (config 2), fp64, N = 2^20, tiled SoA (tile 4096), plan-specialised kernel"),
-    "ik32s": ("kinhip_jit_ik_6_4_f32", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
-              "config 4: DLS IK, 65,536 targets, 64 iterations, 3 restarts, G = 4, fp32, plan-specialised kernel"),
+    "ik32s": ("kinhip_jit_ik_6_", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
+              "config 4: DLS IK, 65,536 targets, 64 iterations, 3 restarts, fp32, plan-specialised kernels; one solve "
+              "= the two-phase schedule's two launches (ik_6_1: attempt 0 of every target, G = 1; ik_6_4: the other "
+              "attempts of the unsolved targets, G = 4), counters and durations summed over both"),
     "coll32s": ("kinhip_jit_coll_0_f32", (8 + 1) * 4 * (1 << 20),
                 "config 5 validity: FK + 14 spheres vs 7-box fridge SDF, min distance, fp32, N = 2^20, specialised"),
     "collg32s": ("kinhip_jit_coll_1_f32", (8 + 14 + 14 * 8) * 4 * (1 << 20),
@@ -115,20 +117,31 @@ def recompute(paths):
 
 
 def counters(tag):
+    """Per-launch mean of each counter per matching kernel, summed over the matching kernels (a
+    workload whose one unit of work is several launches, e.g. the two-phase IK solve)."""
     agg = collections.defaultdict(list)
     kern = WORK[tag][0]
     for f in glob.glob(os.path.join(PROF, f"{tag}_*", "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if kern in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}
+                agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    out = collections.defaultdict(float)
+    for (_, k), v in agg.items():
+        out[k] += sum(v) / len(v)
+    return dict(out)
 
 
 def stats(path, kern):
-    for r in csv.DictReader(open(path)):
-        if kern in r["Name"]:
-            return {k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "StdDev")}
-    return None
+    """Kernel-stats row of the matching kernel; several matching kernels (one unit of work = several
+    launches) are summed: AverageNs = the sum of their average durations."""
+    rows = [r for r in csv.DictReader(open(path)) if kern in r["Name"]]
+    if not rows:
+        return None
+    if len(rows) == 1:
+        return {k: rows[0][k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "StdDev")}
+    return {"Name": " + ".join(r["Name"] for r in rows), "Calls": rows[0]["Calls"],
+            "AverageNs": str(sum(float(r["AverageNs"]) for r in rows)),
+            "per_kernel_avg_ns": {r["Name"]: float(r["AverageNs"]) for r in rows}}
 
 
 def main():
@@ -156,6 +169,7 @@ def main():
              "traffic_over_algorithmic": (hbm / alg) if hbm else None,
              "fetch_size_kb_raw": c.get("FETCH_SIZE"), "write_size_kb": c.get("WRITE_SIZE"),
              "avg_duration_ns_trace": float(st["AverageNs"]) if st else None,
+             "per_kernel_avg_ns": st.get("per_kernel_avg_ns") if st else None,
              "achieved_GBs_trace": (alg / float(st["AverageNs"])) if st else None,
              "sq": {k: v for k, v in c.items() if k.startswith(("SQ_", "GRBM_"))},
              "valu": valu_metrics(c),
