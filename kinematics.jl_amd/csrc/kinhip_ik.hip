@@ -81,6 +81,12 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         const char* e = getenv("KINHIP_IK_TWO_PHASE");
         return e ? atoi(e) : -1;
     }();
+    // KINHIP_IK_TP_QUEUE=<0|1> (A/B): phase 1 of a large batch on wave-local queues; default:
+    // automatic (only where the queue's resident waves do not lower the kernel's occupancy)
+    static const int tpq_env = [] {
+        const char* e = getenv("KINHIP_IK_TP_QUEUE");
+        return e ? atoi(e) : -1;
+    }();
     auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw) -> hipError_t {
         const dim3 grid((unsigned)((nw * 64 + 255) / 256)), block(256);
         const T* tc = target + s0;
@@ -131,7 +137,23 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a1.phase1 = 1;
             a1.fail_list = scr.fail_list;
             a1.fail_n = scr.fail_n;
-            if ((e = one(a1, 1, s0, c, 64, (c + 63) / 64)) != hipSuccess) return e;
+            // phase 1 shares out targets like the one-phase schedule (one per lane while the batch
+            // fills the chip in at most two rounds of waves, else wave-local queues) -- but a queue
+            // of `resident_waves` waves must not run fewer waves per CU than the kernel could hold:
+            // where the hardware keeps more resident (the fp32 specialised kernel, 3 per SIMD), the
+            // full grid backfilled by the dispatcher is faster (profiles/r02_ik_queue_ab.txt)
+            const int64_t plain1 = (c + 63) / 64;
+            bool q1 = tpq_env != 0 && (qmode >= 0 ? qmode != 0 : plain1 > 2 * resident_waves);
+            if (q1 && tpq_env < 0 && qmode < 0 && jf) {
+                const hipFunction_t f1 = jf->ik[a.with_rot ? 1 : 0][0];
+                int nb = 0;
+                if (f1 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f1, 256, 0) == hipSuccess &&
+                    (int64_t)nb * 4 * cus > resident_waves)
+                    q1 = false;
+            }
+            const int64_t w1 = q1 ? std::min(resident_waves, plain1) : plain1;
+            const int64_t pw1 = (c + w1 - 1) / w1;
+            if ((e = one(a1, 1, s0, c, pw1, (c + pw1 - 1) / pw1)) != hipSuccess) return e;
             IkArgsT<T> a2 = at;  // phase 2: attempts 1.. of the listed targets, side by side
             a2.att0 = 1;
             a2.idx = scr.fail_list;

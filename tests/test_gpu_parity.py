@@ -481,6 +481,26 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_ik_dls_two_phase_large_identical(dev, dtype):
+    """A batch of more than two rounds of resident waves (2^19 targets): phase 1 may run on wave-local
+    queues (automatic where that does not lower the kernel's occupancy -- fp64 here, not fp32);
+    angles, iteration counts and errors equal the one-phase schedule (lanes=4) bit for bit."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    plan.specialize()
+    N = 1 << 19
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=77,
+                                dtype=dtype, device=dev)
+    T = plan.run(Qt)[0][0].contiguous()
+    kw = dict(max_iters=64, restarts=3, seed=3, lam=1e-2, max_step=0.5)
+    a = plan.ik_dls(T, torch.zeros((8, N), dtype=dtype, device=dev), lanes=0, **kw)
+    b = plan.ik_dls(T, torch.zeros((8, N), dtype=dtype, device=dev), lanes=4, **kw)
+    assert (a[1] > 16).any() and (a[1] <= 64).float().mean() > 0.99  # phase 2 did work; solves converge
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
 def test_ik_dls_work_queue_identical(dev, fetch_tree):
     """Large batches run as per-wave work queues (a lane group that finishes takes the wave's next
     target): bit-identical to one target per group (lanes=1 here never queues), and the first
