@@ -257,7 +257,10 @@ typedef struct kin_ik_params {
                            launches: attempt 0 of every target, then the remaining attempts of the
                            targets attempt 0 did not solve, side by side (same results).  The two-phase
                            scratch (first call: hipMalloc, synchronising) is per plan, with 4 sets used in
-                           turn: at most 4 such calls of one plan may be in flight at once. */
+                           turn: calls on one stream are always safe; at most 4 calls of one plan may run
+                           concurrently on different streams (a captured graph keeps the set of its
+                           captured call).  Beyond that, pass lanes > 0 (one phase) or use one plan per
+                           stream. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */
