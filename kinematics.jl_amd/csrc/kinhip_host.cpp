@@ -1400,14 +1400,17 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
             std::lock_guard<std::mutex> lk(p->ik_mu);
             if (!p->d_ikscr) {
                 hipError_t e0 = hipMalloc(&p->d_ikscr, set_bytes * kin_plan::kIkScratchSets);
+                // the rings' control words start at zero and are never reset afterwards (launch_ik_dls)
+                if (e0 == hipSuccess) e0 = hipMemset(p->d_ikscr, 0, set_bytes * kin_plan::kIkScratchSets);
                 if (e0 != hipSuccess) {
+                    if (p->d_ikscr) (void)hipFree(p->d_ikscr);
                     p->d_ikscr = nullptr;
                     return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e0));
                 }
             }
         }
         unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * (p->ik_seq.fetch_add(1) % kin_plan::kIkScratchSets);
-        scr.fail_n = (uint32_t*)base;
+        scr.fail_ctl = (uint32_t*)base;
         scr.fail_list = (int32_t*)(base + 256);
         scr.cap = kin_plan::kIkScratchCap;
     }

@@ -50,7 +50,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
     const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
-                  0, 0, 0, nullptr, nullptr, nullptr};
+                  0, 0, 0, nullptr, nullptr, nullptr, 0u};
     const int G = ik_group(n, natt, a.lanes);
     static const int cus = [] {
         int dev = 0, c = 0;
@@ -75,7 +75,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     // chip only by running the restart attempts of a target side by side (G lanes), and a wave then
     // lasts as long as any of its targets' attempts.  Phase 1 runs attempt 0 of every target on one
     // lane and writes the solved ones; phase 2 runs attempts 1, 2, ... side by side for the ones
-    // attempt 0 did not solve, packed densely (fail_list).  Each attempt's arithmetic is unchanged
+    // attempt 0 did not solve, packed densely (fail_list, a ring: IkArgsT).  Each attempt's arithmetic is unchanged
     // and the lowest converged attempt is still the one written: results are identical.
     static const int tp_env = [] {
         const char* e = getenv("KINHIP_IK_TWO_PHASE");
@@ -130,13 +130,14 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         const bool two = scr.fail_list && natt > 1 && c <= scr.cap && a.lanes == 0 &&
                          (tp_env >= 0 ? tp_env != 0 : plain > resident_waves);
         if (two) {
-            hipError_t e = hipMemsetAsync(scr.fail_n, 0, sizeof(uint32_t), st);
-            if (e != hipSuccess) return e;
+            // the ring's control words carry over from the previous call (no reset launch)
+            hipError_t e;
             IkArgsT<T> a1 = at;  // phase 1: attempt 0, one lane per target
             a1.n_attempts = 1;
             a1.phase1 = 1;
             a1.fail_list = scr.fail_list;
-            a1.fail_n = scr.fail_n;
+            a1.fail_ctl = scr.fail_ctl;
+            a1.fail_mask = (uint32_t)(scr.cap - 1);
             // phase 1 shares out targets like the one-phase schedule (one per lane while the batch
             // fills the chip in at most two rounds of waves, else wave-local queues) -- but a queue
             // of `resident_waves` waves must not run fewer waves per CU than the kernel could hold:
@@ -157,10 +158,15 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             IkArgsT<T> a2 = at;  // phase 2: attempts 1.. of the listed targets, side by side
             a2.att0 = 1;
             a2.idx = scr.fail_list;
-            a2.fail_n = scr.fail_n;
+            a2.fail_ctl = scr.fail_ctl;
+            a2.fail_mask = (uint32_t)(scr.cap - 1);
             const int G2 = natt - 1 <= 1 ? 1 : natt - 1 <= 2 ? 2 : natt - 1 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
-            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) return e;
+            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
+                // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring
+                (void)hipMemsetAsync(scr.fail_ctl, 0, 3 * sizeof(uint32_t), st);
+                return e;
+            }
             continue;
         }
         const bool queue = qmode >= 0 ? qmode != 0 : plain > 2 * resident_waves;

@@ -115,13 +115,20 @@ struct IkArgsT {
     int64_t ibase;  // global index of this chunk's first configuration
     // Two-phase schedule (launch_ik_dls, small batches): phase 1 runs attempt 0 of every target
     // (one lane each) and appends the targets it does not solve to fail_list instead of writing
-    // them; phase 2 runs attempts att0 = 1, 2, ... of the listed targets only (idx = fail_list,
-    // *fail_n of them).  Otherwise att0 = 0, phase1 = 0, idx = null.
+    // them; phase 2 runs attempts att0 = 1, 2, ... of the listed targets only (idx = fail_list).
+    // Otherwise att0 = 0, phase1 = 0, idx = null.
+    // fail_list is a ring of fail_mask + 1 entries with three control words that are never reset
+    // between calls (so no memset launch precedes phase 1, and a captured graph replays as is):
+    // fail_ctl[0] = ring head (phase 1 appends at atomicAdd(head) & mask), fail_ctl[1] = this
+    // call's first entry (phase 1 copies it from fail_ctl[2]), fail_ctl[2] = the next call's
+    // first entry (phase 2 sets it to the head, after every phase-1 append).  Phase 2's targets
+    // are the entries [fail_ctl[1], fail_ctl[0]).
     int32_t att0;
     int32_t phase1;
     const int32_t* idx;
     int32_t* fail_list;
-    uint32_t* fail_n;
+    uint32_t* fail_ctl;
+    uint32_t fail_mask;
 };
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
@@ -183,7 +190,13 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const int lane = (int)(threadIdx.x & 63u);
     const int slot = lane % G, grp = lane / G;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nt = a.idx ? (int64_t)*a.fail_n : n;  // phase 2: the listed targets only
+    // two-phase control words (see IkArgsT): one lane of the grid moves the ring's start marks
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (a.phase1) a.fail_ctl[1] = a.fail_ctl[2];
+        else if (a.idx) a.fail_ctl[2] = a.fail_ctl[0];
+    }
+    const uint32_t fbeg = a.idx ? a.fail_ctl[1] : 0u;
+    const int64_t nt = a.idx ? (int64_t)(uint32_t)(a.fail_ctl[0] - fbeg) : n;  // phase 2: the listed targets only
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
     int64_t i = 0;
@@ -231,7 +244,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         if (gfin) {
             const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
             if (a.phase1 && res_att == INT_MAX) {  // attempt 0 failed: phase 2 takes the target
-                a.fail_list[atomicAdd(a.fail_n, 1u)] = (int32_t)i;
+                a.fail_list[atomicAdd(&a.fail_ctl[0], 1u) & a.fail_mask] = (int32_t)i;
             } else if (writer) {
 #pragma unroll
                 for (int s2 = 0; s2 < MAXA; ++s2) {
@@ -253,7 +266,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             const uint64_t lead = 1ull << (grp * G);
             const int rank = __popcll(need & (lead - 1ull));
             if (!have && (need & lead) && next + rank < wend) {
-                i = a.idx ? (int64_t)a.idx[next + rank] : next + rank;
+                i = a.idx ? (int64_t)a.idx[(fbeg + (uint32_t)(next + rank)) & a.fail_mask] : next + rank;
                 have = true;
                 start_target();  // the single (inlined) initialisation site
             }

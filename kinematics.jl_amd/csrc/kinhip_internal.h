@@ -54,8 +54,8 @@ struct IkArgs {
 // not solve and its length, for batches of up to `cap` targets (null: single phase only)
 struct IkScratch {
     int32_t* fail_list = nullptr;
-    uint32_t* fail_n = nullptr;
-    int64_t cap = 0;
+    uint32_t* fail_ctl = nullptr;  // 3 control words of the ring (IkArgsT), zero at allocation
+    int64_t cap = 0;               // ring entries, a power of two
 };
 
 template <typename T>
