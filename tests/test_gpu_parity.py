@@ -481,6 +481,40 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
+def test_ik_dls_two_phase_graph_replay(dev):
+    """The two-phase schedule's scratch is a ring whose control words carry over between calls (no
+    reset launch): a hipGraph captured around one call replays it any number of times, interleaved
+    with eager calls of the same plan on the same stream, with the eager call's results bit for bit."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+    plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    N = 1 << 16
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=91,
+                                dtype=torch.float32, device=dev)
+    T = plan.run(Qt)[0][0].contiguous()
+    kw = dict(max_iters=64, restarts=3, seed=9, lam=1e-2, max_step=0.5)
+    Q0 = torch.zeros((8, N), dtype=torch.float32, device=dev)
+    ref = plan.ik_dls(T, Q0.clone(), **kw)  # eager; also allocates the plan's scratch before capture
+    ref = [t.clone() for t in ref]
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    Qg = Q0.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            Qg.copy_(Q0)
+            out = plan.ik_dls(T, Qg, stream=s, **kw)
+        for rep in range(3):
+            g.replay()
+            s.synchronize()
+            assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]) and torch.equal(out[2], ref[2]), rep
+            e = plan.ik_dls(T, Q0.clone(), stream=s, **kw)  # eager calls rotate through the other sets
+            s.synchronize()
+            assert torch.equal(e[0], ref[0]) and torch.equal(e[1], ref[1]), rep
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_ik_dls_two_phase_large_identical(dev, dtype):
     """A batch of more than two rounds of resident waves (2^19 targets): phase 1 may run on wave-local
