@@ -136,15 +136,16 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=20, spec=1, dt=torch.float32)
     tgt, kw = ik_shard(m, arm, gl, ctx, n, dt)
     cnt = tgt.shape[1]
     Q0 = torch.zeros((8, cnt), dtype=dt, device=ctx.device)
+    # every batch starts from Q0: read by the solver (kin_ik_dls_batch_from), the solutions go to a
+    # fresh Q (written, not read) -- no copy of Q0 per batch
     with torch.cuda.stream(stream):
-        plan.ik_dls(tgt, Q0.clone(), stream=stream, **kw)
+        plan.ik_dls(tgt, torch.empty_like(Q0), stream=stream, Q0=Q0, **kw)
     torch.cuda.synchronize()
     D.barrier(ctx)
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
         for _ in range(reps):
-            Q = Q0.clone()
-            Q, it, err = plan.ik_dls(tgt, Q, stream=stream, **kw)
+            Q, it, err = plan.ik_dls(tgt, torch.empty_like(Q0), stream=stream, Q0=Q0, **kw)
     torch.cuda.synchronize()
     D.barrier(ctx)
     wall = D.max_over_ranks(ctx, [time.perf_counter() - t0])[0]

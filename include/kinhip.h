@@ -268,6 +268,15 @@ typedef struct kin_ik_params {
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,
                                 void* stream);
+/* kin_ik_dls_batch with the starting angles read from q0 ([n_q][ldq], same leading dimension as q,
+ * not modified) instead of q: the chain's columns (and base columns) of q are written for every
+ * target without being read, other columns of q are left as they are.  Same results as copying q0
+ * into q and calling kin_ik_dls_batch, without the copy; lets a caller solve many target batches
+ * from one q0 (the reference's inverse_kinematics! starts from the mechanism's current angles,
+ * src/inverse_kinematics.jl:32-64).  q0 == q is the in-place call; other overlaps are not allowed. */
+KINHIP_API int kin_ik_dls_batch_from(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
+                                     const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* err,
+                                     int64_t lde, void* stream);
 
 /* point_inverse_kinematics_nakamura (src/algorithm.jl:116-131), batched:
  * 50 SR-inverse iterations, `.+ sr_weight` broadcast quirk reproduced.

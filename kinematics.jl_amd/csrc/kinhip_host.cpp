@@ -1370,8 +1370,8 @@ int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, con
     return KIN_OK;
 }
 
-int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, void* q,
-                     int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
+static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, const void* q0,
+                        void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
     if (!p || !prm) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: null argument");
     if (!p->ik_ok) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: plan not usable for IK: " + p->ik_why);
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
@@ -1417,12 +1417,24 @@ int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* ta
     hipError_t e;
     if (p->dtype == KIN_F32)
         e = launch_ik_dls<float>(p->pf, (const KStep<float>*)p->d_steps, p->geom, a, (const float*)target, ldt,
-                                 (float*)q, ldq, n, iters, (float*)err, lde, jf, scr, (hipStream_t)stream);
+                                 (const float*)q0, (float*)q, ldq, n, iters, (float*)err, lde, jf, scr, (hipStream_t)stream);
     else
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
-                                  (double*)q, ldq, n, iters, (double*)err, lde, jf, scr, (hipStream_t)stream);
+                                  (const double*)q0, (double*)q, ldq, n, iters, (double*)err, lde, jf, scr,
+                                  (hipStream_t)stream);
     if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
     return KIN_OK;
+}
+
+int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, void* q,
+                     int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
+    return ik_dls_batch(p, prm, target, ldt, nullptr, q, ldq, n, iters, err, lde, stream);
+}
+
+int kin_ik_dls_batch_from(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, const void* q0,
+                          void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
+    if (!q0) return set_error(KIN_E_INVALID, "kin_ik_dls_batch_from: null q0");
+    return ik_dls_batch(p, prm, target, ldt, q0 == q ? nullptr : q0, q, ldq, n, iters, err, lde, stream);
 }
 
 int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt, void* q, int64_t ldq, int64_t n,

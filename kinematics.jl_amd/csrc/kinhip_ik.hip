@@ -45,12 +45,12 @@ static int ik_group(int64_t n, int n_attempts, int lanes) {
 
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
-                         const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st) {
+                         const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
+                         T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st) {
     const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
     const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
-                  0, 0, 0, nullptr, nullptr, nullptr, 0u};
+                  0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr};
     const int G = ik_group(n, natt, a.lanes);
     static const int cus = [] {
         int dev = 0, c = 0;
@@ -122,6 +122,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = a.index_base + s0;
+        at.q0 = q0 ? q0 + s0 : nullptr;
         const int64_t c = std::min(chunk, n - s0);
         const int64_t ng = 64 / G;
         const int64_t plain = (c + ng - 1) / ng;
@@ -205,7 +206,7 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
 
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, \
-                                         const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,     \
+                                         const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t, \
                                          const JitFns*, const IkScratch&, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
                                            int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);

@@ -129,6 +129,9 @@ struct IkArgsT {
     int32_t* fail_list;
     uint32_t* fail_ctl;
     uint32_t fail_mask;
+    // starting angles (kin_ik_dls_batch_from): read from q0 (same leading dimension as q) instead of
+    // q, so q is written without being read and a caller keeps q0 for the next batch; null: q in place
+    const T* q0;
 };
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
@@ -196,6 +199,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         else if (a.idx) a.fail_ctl[2] = a.fail_ctl[0];
     }
     const uint32_t fbeg = a.idx ? a.fail_ctl[1] : 0u;
+    const T* __restrict__ qin = a.q0 ? a.q0 : q;  // uniform: where the starting angles are read
     const int64_t nt = a.idx ? (int64_t)(uint32_t)(a.fail_ctl[0] - fbeg) : n;  // phase 2: the listed targets only
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
@@ -220,7 +224,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
         b0[0] = b0[1] = b0[2] = T(0);
         if (base)
-            for (int k = 0; k < 3; ++k) b0[k] = KIN_IK_LD(q, P.base_col + k, ldq, off);
+            for (int k = 0; k < 3; ++k) b0[k] = KIN_IK_LD(qin, P.base_col + k, ldq, off);
         b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
         att = a.att0 + slot;
         done = att >= a.n_attempts;
@@ -228,7 +232,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         final_lane = false;
         it = att > 0 ? att * L + 1 : 0;
         ep = er = T(0);
-        ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
+        ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
     };
     T ro[MAXA][3], rz[MAXA][3];
     for (;;) {
@@ -306,7 +310,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 done = true;
             } else {
                 it = att * L + 1;
-                ik_start_attempt<T, MAXA>(S, a, q, ldq, off, a.ibase + i, att, qs);
+                ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
                 b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
             }
             continue;

@@ -60,8 +60,8 @@ struct IkScratch {
 
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
-                         const T* target, int64_t ldt, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err,
-                         int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st);
+                         const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
+                         T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st);
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,

@@ -220,6 +220,27 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
     Q, iters, err
 end
 
+"""Batched IK from the seeds Q0 (N, dof; not modified) into Q (written, not read): the same results as
+copyto!(Q, Q0) followed by inverse_kinematics!, without the copy (kin_ik_dls_batch_from)."""
+function inverse_kinematics_from!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
+                                  Q0::ROCMatrix{T}, Q::ROCMatrix{T}; max_iters=64, lambda=1e-2, tol_pos=1e-3,
+                                  tol_rot=1e-3, max_step=0.5, with_rot=true, restarts=0, seed=0, lanes=0,
+                                  index_base=0) where {T}
+    N = size(Q, 1)
+    size(Q0) == size(Q) && stride(Q0, 2) == stride(Q, 2) || throw(DimensionMismatch("Q0 and Q differ in shape"))
+    ids = Int32[j.id for j in joints]
+    p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
+    iters = ROCVector{Int32}(undef, N)
+    err = ROCMatrix{T}(undef, N, 2)
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, with_rot, restarts, seed, lanes, index_base)
+    check(ccall((:kin_ik_dls_batch_from, libkinhip), Cint,
+                (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T},
+                 Int64, Ptr{Cvoid}),
+                p, prm, pointer(targets), stride(targets, 2), pointer(Q0), pointer(Q), stride(Q, 2), N,
+                pointer(iters), pointer(err), N, stream_ptr()))
+    Q, iters, err
+end
+
 function point_inverse_kinematics_nakamura!(hm::HIPModel, link::Link, joints::Vector{<:Joint},
                                             points::ROCMatrix{T}, Q::ROCMatrix{T}) where {T}
     N = size(Q, 1)

@@ -35,7 +35,7 @@ EXPORTS = [
     "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run", "kin_plan_run_tiled",
     "kin_plan_specialize", "kin_plan_specialized", "kin_jit_selfcheck",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
-    "kin_ik_dls_batch", "kin_point_ik_nakamura_batch",
+    "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch", "kin_coll_batch_tiled",
     "kin_ineq_const_batch", "kin_ineq_const_batch_tiled", "kin_pose_const_batch",
 ]
@@ -117,6 +117,7 @@ def lib():
         "kin_get_transform_batch": ([P, I32, I32, P, P, I64, I64, I32, P, P, I64, P], C.c_int),
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),
         "kin_ik_dls_batch": ([P, P, P, I64, P, I64, I64, P, P, I64, P], C.c_int),
+        "kin_ik_dls_batch_from": ([P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_point_ik_nakamura_batch": ([P, P, I64, P, I64, I64, P], C.c_int),
         "kin_sdf_create_boxes": ([I32, P, P, P], C.c_int),
         "kin_sdf_destroy": ([P], C.c_int),

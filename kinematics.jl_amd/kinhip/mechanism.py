@@ -331,14 +331,21 @@ class Plan:
         return poses, jac
 
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None):
+               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None, Q0=None):
         """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
         target running restart attempts side by side (0 auto, which runs batches of more than one round
         of waves in two phases: attempt 0 of every target, then the other attempts of the unsolved ones;
         results identical for every value).
         `index_base`: global index of target 0 for the restart draws (a shard's offset), so a target
-        set sharded over ranks solves exactly as in one process.  iters > max_iters: not converged."""
+        set sharded over ranks solves exactly as in one process.  iters > max_iters: not converged.
+        `Q0`: starting angles read from Q0 (same shape and strides as Q, not modified) and Q written
+        without being read (``kin_ik_dls_batch_from``): the results of ``Q.copy_(Q0)`` + the in-place
+        call, without the copy."""
         N = self._check_q(Q)
+        if Q0 is not None:
+            _same_device(Q0, Q, "Q0")
+            if Q0.shape != Q.shape or Q0.stride() != Q.stride() or Q0.dtype != Q.dtype:
+                raise ValueError("Q0 must have Q's shape, strides and dtype")
         if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
             raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
         _same_device(targets, Q, "targets")
@@ -347,8 +354,13 @@ class Plan:
         prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
                          int(restarts), int(seed), int(lanes), int(index_base))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
-        K.check(K.lib().kin_ik_dls_batch(self._h, C.byref(prm), targets.data_ptr(), N, Q.data_ptr(), Q.stride(0), N,
-                                         iters.data_ptr(), err.data_ptr(), N, st))
+        if Q0 is not None:
+            K.check(K.lib().kin_ik_dls_batch_from(self._h, C.byref(prm), targets.data_ptr(), N, Q0.data_ptr(),
+                                                  Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N,
+                                                  st))
+        else:
+            K.check(K.lib().kin_ik_dls_batch(self._h, C.byref(prm), targets.data_ptr(), N, Q.data_ptr(), Q.stride(0),
+                                             N, iters.data_ptr(), err.data_ptr(), N, st))
         return Q, iters, err
 
     def point_ik_nakamura(self, points: torch.Tensor, Q: torch.Tensor, stream=None):

@@ -10,8 +10,9 @@ hipError_t launch_fk(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const 
     return hipErrorNoDevice;
 }
 template <typename T>
-hipError_t launch_ik_dls(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, const T*, int64_t, T*,
-                         int64_t, int64_t, int32_t*, T*, int64_t, const JitFns*, const IkScratch&, hipStream_t) {
+hipError_t launch_ik_dls(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&, const T*, int64_t,
+                         const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t, const JitFns*, const IkScratch&,
+                         hipStream_t) {
     return hipErrorNoDevice;
 }
 template <typename T>
@@ -33,7 +34,7 @@ hipError_t launch_pose_residual(const T*, int64_t, const T*, int64_t, int64_t, i
     template hipError_t launch_fk<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t,        \
                                      int64_t, T*, int64_t, T*, int64_t, const TileArgs&, const JitFns*, hipStream_t); \
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&,        \
-                                         const T*, int64_t, T*, int64_t, int64_t, int32_t*, T*, int64_t,            \
+                                         const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t,  \
                                          const JitFns*, const IkScratch&, hipStream_t);                              \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, \
                                            T*, int64_t, int64_t, const JitFns*, hipStream_t);                       \

@@ -481,6 +481,35 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
+@pytest.mark.parametrize("dtype,N,lanes", [(torch.float32, 1 << 16, 0), (torch.float64, 1 << 16, 0),
+                                             (torch.float32, 3000, 4), (torch.float64, 3000, 1)])
+def test_ik_dls_from_q0_identical(dev, dtype, N, lanes):
+    """kin_ik_dls_batch_from (starting angles read from Q0, Q written without being read) returns the
+    in-place call's angles, iteration counts and errors bit for bit -- two-phase (65,536 targets) and
+    one-phase schedules -- leaves Q0 unchanged, and q0 == q is the in-place call."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    lo, hi = [j.lower_limit for j in arm], [j.upper_limit for j in arm]
+    T = plan.run(kinhip.uniform_configs(lo, hi, N, seed=31, dtype=dtype, device=dev))[0][0].contiguous()
+    Q0 = kinhip.uniform_configs(lo, hi, N, seed=32, dtype=dtype, device=dev) * 0.5
+    keep = Q0.clone()
+    kw = dict(max_iters=64, restarts=3, seed=4, lam=1e-2, max_step=0.5, lanes=lanes)
+    ref = plan.ik_dls(T, Q0.clone(), **kw)
+    out = plan.ik_dls(T, torch.full_like(Q0, float("nan")), Q0=Q0, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(Q0, keep)
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)
+    Qs = Q0.clone()
+    same = plan.ik_dls(T, Qs, Q0=Qs, **kw)  # q0 == q: in place
+    for a, b in zip(same, ref):
+        assert torch.equal(a, b)
+    with pytest.raises(ValueError):
+        plan.ik_dls(T, torch.empty((8, N + 1), dtype=dtype, device=dev), Q0=Q0, **kw)
+
+
 def test_ik_dls_two_phase_graph_replay(dev):
     """The two-phase schedule's scratch is a ring whose control words carry over between calls (no
     reset launch): a hipGraph captured around one call replays it any number of times, interleaved
