@@ -144,6 +144,16 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
 #define KINHIP_COLL_PAIRS 1
 #endif
 
+// Paired gradient stores (A/B knob, specialised fp32 kernels only): the two lanes of a pair swap one
+// value and each writes two configurations of one row with a 64-bit store (rows c and c + 1 of a
+// sphere), half the store instructions of one row per lane.  Full waves, ndof <= 16, even ld only.
+#ifndef KINHIP_COLL_STPAIR
+#define KINHIP_COLL_STPAIR 0
+#endif
+#ifndef KINHIP_JIT
+#define KINHIP_JIT 0
+#endif
+
 template <typename T, int MAXA, bool GRAD>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
                                              const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
@@ -154,6 +164,9 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              T* __restrict__ grads, int64_t ldg, T& dmin,
                                              const unsigned char* smem, bool use_lds) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
+    // paired stores (KINHIP_COLL_STPAIR): every lane of the wave active, rows 8-byte aligned
+    const bool pair_ok = GRAD && KINHIP_COLL_STPAIR && grads && (ldg & 1) == 0 &&
+                         (((uint64_t)grads) & 7u) == 0 && __ballot(1) == ~0ull;
     // sphere centre in the world (fmz: in specialised kernels the centre is a constant, often with
     // zero components)
     auto centre = [&](const KSphere<T>& sp, T& px, T& py, T& pz) {
@@ -189,6 +202,53 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         d -= offs;  // IneqConst: dist - margin (src/planning.jl:66)
         dmin = fmin(dmin, d);
         if (dists) st_soa(dists, sp.out, ldd, off, d);
+        if constexpr (GRAD && KINHIP_COLL_STPAIR && KINHIP_JIT && sizeof(T) == 4) {
+            constexpr int NC = 16;
+            if (ndof <= NC && pair_ok) {  // uniform
+                const int64_t r0 = (int64_t)sp.out * ndof;
+                T cv[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) cv[c] = T(0);  // and the columns that cannot move this chain
+                const T w0 = fma(py, g[2], -(pz * g[1])), w1 = fma(pz, g[0], -(px * g[2])), w2 = fma(px, g[1], -(py * g[0]));
+#pragma unroll
+                for (int j = 0; j < MAXA; ++j) {
+                    if (S[j].flags & SF_REC) {
+                        T v = T(0);
+                        if (j <= s_last && !cut) {
+                            if (S[j].jkind == MOT_PRISM)
+                                v = fma(g[0], rz[j][0], fma(g[1], rz[j][1], g[2] * rz[j][2]));
+                            else
+                                v = fma(rz[j][0], w0, fma(rz[j][1], w1, fma(rz[j][2], w2,
+                                    -fma(g[0], rm[j][0], fma(g[1], rm[j][1], g[2] * rm[j][2])))));
+                        }
+#pragma unroll
+                        for (int c = 0; c < NC; ++c)
+                            if ((S[j].colmask >> c) & 1ull) cv[c] = v;
+                    }
+                }
+                if (P.flags & PF_BASE) {
+#pragma unroll
+                    for (int c = 0; c < NC; ++c) {
+                        if (c == P.n_jac) cv[c] = cut ? T(0) : g[0];
+                        if (c == P.n_jac + 1) cv[c] = cut ? T(0) : g[1];
+                        if (c == P.n_jac + 2) cv[c] = cut ? T(0) : fma(-g[0], py - by, g[1] * (px - bx));
+                    }
+                }
+                const int par = (int)(threadIdx.x & 1u);
+#pragma unroll
+                for (int c = 0; c < NC; c += 2) {
+                    if (c + 1 < ndof) {
+                        const T send = par ? cv[c] : cv[c + 1];
+                        const T recv = __shfl_xor(send, 1);
+                        st_soa2(grads, r0 + c + par, ldg, off - (uint32_t)par * 4u, par ? recv : cv[c],
+                                par ? cv[c + 1] : recv);
+                    } else if (c < ndof) {
+                        st_soa(grads, r0 + c, ldg, off, cv[c]);
+                    }
+                }
+                return;
+            }
+        }
         if (GRAD) {
             const int64_t r0 = (int64_t)sp.out * ndof;
             uint64_t zm = P.zmask;  // q columns that cannot move this chain: 0

@@ -170,6 +170,11 @@ __device__ __forceinline__ double ld_soa(const double* __restrict__ base, int64_
 __device__ __forceinline__ void st_soa(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base + row * ld), (int)off, 0, KINHIP_STORE_AUX);
 }
+// two consecutive configurations of one row (8 bytes at off, 8-byte aligned)
+__device__ __forceinline__ void st_soa2(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float lo, float hi) {
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(lo), __float_as_uint(hi)}, row_rsrc(base + row * ld),
+                                          (int)off, 0, KINHIP_STORE_AUX);
+}
 __device__ __forceinline__ void st_soa(double* __restrict__ base, int64_t row, int64_t ld, uint32_t off, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), row_rsrc(base + row * ld), (int)off, 0,
                                           KINHIP_STORE_AUX);
