@@ -73,8 +73,7 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
     // profiles/r02_fk_stride_ab.txt).
     // KINHIP_FK_PER_LANE=<k> forces k configurations per lane (1: the plain kernel).
     static const int per_lane_env = [] {
-        const char* e = getenv("KINHIP_FK_PER_LANE");
-        const int v = e ? atoi(e) : 0;
+        const int v = ab_env_int("KINHIP_FK_PER_LANE", 0);
         return v >= 1 && v <= 64 ? v : 0;
     }();
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk

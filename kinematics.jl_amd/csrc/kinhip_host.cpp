@@ -197,14 +197,19 @@ struct kin_plan {
     int32_t n_steps = 0;
     JitKernels* jit = nullptr;
     uint32_t jit_mask = 0;
-    // two-phase IK schedule scratch (launch_ik_dls): allocated at the first kin_ik_dls_batch call;
-    // kIkScratchSets sets used in turn, so launches of one plan on several streams at once do not
-    // share a list (up to kIkScratchSets in flight)
-    static constexpr int kIkScratchSets = 4;
+    // two-phase IK schedule scratch (launch_ik_dls): allocated by the first kin_ik_dls_batch call that
+    // runs the two-phase schedule.  Eager calls use sets 0..kIkEagerSets-1 in turn (launches of one
+    // plan on several streams at once do not share a list, up to kIkEagerSets in flight); a call
+    // made inside a stream capture takes one of the remaining sets for good (the captured graph
+    // replays with it, so it never meets an eager call or another graph), and once those are gone
+    // further captures run the one-phase schedule (same results, no scratch).
+    static constexpr int kIkScratchSets = 8;
+    static constexpr int kIkEagerSets = 4;
     static constexpr int64_t kIkScratchCap = int64_t(1) << 20;
     mutable std::mutex ik_mu;
     mutable void* d_ikscr = nullptr;
     mutable std::atomic<uint32_t> ik_seq{0};
+    mutable int ik_captured = 0;  // sets kIkEagerSets .. kIkEagerSets + ik_captured - 1 belong to graphs
     ~kin_plan() {
         if (d_ikscr) (void)hipFree(d_ikscr);
         jit_destroy(jit);
@@ -1392,13 +1397,22 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     const bool narrow = (12 * ldt + span) * esz < (int64_t(1) << 31) && (p->nqcols * ldq + span) * esz < (int64_t(1) << 31) &&
                         (2 * lde + span) * esz < (int64_t(1) << 31);
     const JitFns* jf = narrow ? jit_fns(p->jit) : nullptr;
-    // two-phase schedule scratch (small batches with restarts; launch_ik_dls)
+    // two-phase schedule scratch (small batches with restarts; launch_ik_dls): only a call that runs
+    // that schedule touches it, so every other call stays allocation-free (capture-safe)
     IkScratch scr;
-    if (prm->restarts > 0 && n <= kin_plan::kIkScratchCap) {
+    if (ik_wants_two_phase(a, n, kin_plan::kIkScratchCap)) {
         const size_t set_bytes = sizeof(int32_t) * kin_plan::kIkScratchCap + 256;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+        const bool capturing = cs == hipStreamCaptureStatusActive;
+        int set = -1;
         {
             std::lock_guard<std::mutex> lk(p->ik_mu);
             if (!p->d_ikscr) {
+                if (capturing)
+                    return set_error(KIN_E_INVALID, "kin_ik_dls_batch: the plan's first two-phase call allocates its "
+                                                    "scratch and cannot run inside a stream capture (make one call "
+                                                    "outside the capture first, or pass lanes > 0)");
                 hipError_t e0 = hipMalloc(&p->d_ikscr, set_bytes * kin_plan::kIkScratchSets);
                 // the rings' control words start at zero and are never reset afterwards (launch_ik_dls)
                 if (e0 == hipSuccess) e0 = hipMemset(p->d_ikscr, 0, set_bytes * kin_plan::kIkScratchSets);
@@ -1408,11 +1422,17 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e0));
                 }
             }
+            if (!capturing)
+                set = (int)(p->ik_seq.fetch_add(1) % kin_plan::kIkEagerSets);
+            else if (kin_plan::kIkEagerSets + p->ik_captured < kin_plan::kIkScratchSets)
+                set = kin_plan::kIkEagerSets + p->ik_captured++;
         }
-        unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * (p->ik_seq.fetch_add(1) % kin_plan::kIkScratchSets);
-        scr.fail_ctl = (uint32_t*)base;
-        scr.fail_list = (int32_t*)(base + 256);
-        scr.cap = kin_plan::kIkScratchCap;
+        if (set >= 0) {  // (no set left for a captured call: one phase)
+            unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * set;
+            scr.fail_ctl = (uint32_t*)base;
+            scr.fail_list = (int32_t*)(base + 256);
+            scr.cap = kin_plan::kIkScratchCap;
+        }
     }
     hipError_t e;
     if (p->dtype == KIN_F32)
@@ -1422,7 +1442,12 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
                                   (const double*)q0, (double*)q, ldq, n, iters, (double*)err, lde, jf, scr,
                                   (hipStream_t)stream);
-    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e));
+    if (e != hipSuccess)
+        return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e) +
+                                           (ik_last_call_partial() ? " (phase 2 failed to launch after phase 1: the "
+                                                                     "outputs of the targets phase 1 did not solve are "
+                                                                     "undefined)"
+                                                                   : ""));
     return KIN_OK;
 }
 

@@ -32,10 +32,7 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
 // every SIMD for small batches, never more than the attempts the schedule has.
 // KINHIP_IK_GROUP=<1|2|4|8> overrides (A/B).
 static int ik_group(int64_t n, int n_attempts, int lanes) {
-    static const int env = [] {
-        const char* e = getenv("KINHIP_IK_GROUP");
-        return e ? atoi(e) : 0;
-    }();
+    static const int env = ab_env_int("KINHIP_IK_GROUP", 0);
     const int forced = lanes ? lanes : env;
     if (forced == 1 || forced == 2 || forced == 4 || forced == 8) return forced;
     int g = 1;
@@ -43,50 +40,76 @@ static int ik_group(int64_t n, int n_attempts, int lanes) {
     return g;
 }
 
-template <typename T>
-hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
-                         const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
-                         T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st) {
-    const int L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
-    const int natt = (L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / L : 1;
-    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
-                  0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr};
-    const int G = ik_group(n, natt, a.lanes);
+static int ik_cus() {
     static const int cus = [] {
         int dev = 0, c = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
         return c > 0 ? c : 256;
     }();
-    // waves per CU that stay resident: 2 per SIMD for the generic kernels (~190-240 VGPRs);
-    // KINHIP_IK_RESIDENT=<waves per CU> overrides (A/B)
-    static const int res_env = [] {
-        const char* e = getenv("KINHIP_IK_RESIDENT");
-        return e ? atoi(e) : 0;
-    }();
-    const int64_t resident_waves = (int64_t)cus * (res_env > 0 ? res_env : 8);
+    return cus;
+}
+
+// waves per CU that stay resident: 2 per SIMD for the generic kernels (~190-240 VGPRs);
+// KINHIP_IK_RESIDENT=<waves per CU> overrides (A/B build only)
+static int64_t ik_resident_waves() {
+    static const int res_env = ab_env_int("KINHIP_IK_RESIDENT", 0);
+    return (int64_t)ik_cus() * (res_env > 0 ? res_env : 8);
+}
+
+static void ik_attempts(const IkArgs& a, int* L, int* natt) {
+    *L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
+    *natt = (*L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / *L : 1;
+}
+
+// Two-phase schedule (KINHIP_IK_TWO_PHASE=<0|1> in the A/B build, default automatic): a chunk of
+// c targets runs in two phases when the caller left the lanes to the engine, there are restart
+// attempts, the chunk fits the scratch ring and it needs more than one round of resident waves at
+// the one-phase schedule's lanes per target.  kin_ik_dls_batch allocates the scratch only when
+// this holds for some chunk of the call (n = the whole call, c = this chunk).
+static bool ik_two_phase(const IkArgs& a, int64_t n, int64_t c, int64_t cap) {
+    static const int tp_env = ab_env_int("KINHIP_IK_TWO_PHASE", -1);
+    int L, natt;
+    ik_attempts(a, &L, &natt);
+    if (natt <= 1 || c > cap || a.lanes != 0) return false;
+    const int64_t ng = 64 / ik_group(n, natt, a.lanes);
+    const int64_t plain = (c + ng - 1) / ng;
+    return tp_env >= 0 ? tp_env != 0 : plain > ik_resident_waves();
+}
+
+bool ik_wants_two_phase(const IkArgs& a, int64_t n, int64_t cap) {
+    for (int64_t s0 = 0; s0 < n; s0 += kIkChunk)
+        if (ik_two_phase(a, n, std::min<int64_t>(kIkChunk, n - s0), cap)) return true;
+    return false;
+}
+
+thread_local bool g_ik_partial = false;
+bool ik_last_call_partial() { return g_ik_partial; }
+
+template <typename T>
+hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
+                         const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
+                         T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st) {
+    int L, natt;
+    ik_attempts(a, &L, &natt);
+    g_ik_partial = false;
+    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
+                  0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr};
+    const int G = ik_group(n, natt, a.lanes);
+    const int cus = ik_cus();
+    const int64_t resident_waves = ik_resident_waves();
     // queue depth: one target per group (no refill) while the batch fills the chip in at most
     // two rounds of waves, else as many waves as stay resident, each working through its share
-    static const int qmode = [] {
-        const char* e = getenv("KINHIP_IK_QUEUE");
-        return e ? atoi(e) : -1;
-    }();
-    // Two-phase schedule (KINHIP_IK_TWO_PHASE=<0|1>, default: automatic): small batches fill the
-    // chip only by running the restart attempts of a target side by side (G lanes), and a wave then
-    // lasts as long as any of its targets' attempts.  Phase 1 runs attempt 0 of every target on one
-    // lane and writes the solved ones; phase 2 runs attempts 1, 2, ... side by side for the ones
-    // attempt 0 did not solve, packed densely (fail_list, a ring: IkArgsT).  Each attempt's arithmetic is unchanged
-    // and the lowest converged attempt is still the one written: results are identical.
-    static const int tp_env = [] {
-        const char* e = getenv("KINHIP_IK_TWO_PHASE");
-        return e ? atoi(e) : -1;
-    }();
+    static const int qmode = ab_env_int("KINHIP_IK_QUEUE", -1);
+    // Two-phase schedule (ik_two_phase): small batches fill the chip only by running the restart
+    // attempts of a target side by side (G lanes), and a wave then lasts as long as any of its
+    // targets' attempts.  Phase 1 runs attempt 0 of every target on one lane and writes the solved
+    // ones; phase 2 runs attempts 1, 2, ... side by side for the ones attempt 0 did not solve, packed
+    // densely (fail_list, a ring: IkArgsT).  Each attempt's arithmetic is unchanged and the lowest
+    // converged attempt is still the one written: results are identical.
     // KINHIP_IK_TP_QUEUE=<0|1> (A/B): phase 1 of a large batch on wave-local queues; default:
     // automatic (only where the queue's resident waves do not lower the kernel's occupancy)
-    static const int tpq_env = [] {
-        const char* e = getenv("KINHIP_IK_TP_QUEUE");
-        return e ? atoi(e) : -1;
-    }();
+    static const int tpq_env = ab_env_int("KINHIP_IK_TP_QUEUE", -1);
     auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw) -> hipError_t {
         const dim3 grid((unsigned)((nw * 64 + 255) / 256)), block(256);
         const T* tc = target + s0;
@@ -128,8 +151,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         const int64_t plain = (c + ng - 1) / ng;
         // (automatic: batches that need more than one round of resident waves at G lanes per target
         // and fit the scratch list; phase 2 runs the remaining attempts side by side)
-        const bool two = scr.fail_list && natt > 1 && c <= scr.cap && a.lanes == 0 &&
-                         (tp_env >= 0 ? tp_env != 0 : plain > resident_waves);
+        const bool two = scr.fail_list && ik_two_phase(a, n, c, scr.cap);
         if (two) {
             // the ring's control words carry over from the previous call (no reset launch)
             hipError_t e;
@@ -164,8 +186,10 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             const int G2 = natt - 1 <= 1 ? 1 : natt - 1 <= 2 ? 2 : natt - 1 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
             if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
-                // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring
+                // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;
+                // the targets phase 1 did not solve keep undefined outputs (kin_ik_dls_batch says so)
                 (void)hipMemsetAsync(scr.fail_ctl, 0, 3 * sizeof(uint32_t), st);
+                g_ik_partial = true;
                 return e;
             }
             continue;

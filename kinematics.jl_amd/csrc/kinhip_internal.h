@@ -2,9 +2,31 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kinhip_prog.h"
 
 namespace kinhip {
+
+// A/B knobs (schedules, occupancy, trig / atan variants, extra compiler options) are read from the
+// environment only by the tools build (`make ab` -> lib/libkinhip_ab.so, -DKINHIP_AB_KNOBS=1,
+// driven by tools/ab.py).  The product library never reads them: a stray environment variable
+// cannot change a drop-in library's schedule or arithmetic.
+#ifndef KINHIP_AB_KNOBS
+#define KINHIP_AB_KNOBS 0
+#endif
+inline const char* ab_env(const char* name) {
+#if KINHIP_AB_KNOBS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+inline int ab_env_int(const char* name, int dflt) {
+    const char* e = ab_env(name);
+    return e ? atoi(e) : dflt;
+}
 
 // phase-A chain bounds compiled into the kernels (kinhip_device.h KIN_MAXA_DISPATCH)
 inline int pick_chain_bound(int n) { return n <= 4 ? 4 : n <= 8 ? 8 : n <= 12 ? 12 : n <= 16 ? 16 : 32; }
@@ -57,6 +79,13 @@ struct IkScratch {
     uint32_t* fail_ctl = nullptr;  // 3 control words of the ring (IkArgsT), zero at allocation
     int64_t cap = 0;               // ring entries, a power of two
 };
+
+// true when some chunk of an n-target kin_ik_dls_batch call runs the two-phase schedule (only then
+// does the call need the plan's scratch ring)
+bool ik_wants_two_phase(const IkArgs& a, int64_t n, int64_t cap);
+// true when the last launch_ik_dls of this thread failed after its phase 1 had been launched (the
+// targets phase 1 did not solve then keep undefined outputs)
+bool ik_last_call_partial();
 
 template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,

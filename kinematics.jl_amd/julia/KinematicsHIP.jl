@@ -86,16 +86,24 @@ joint_type_code(::Kinematics.Joint{Kinematics.Prismatic}) = Int32(2)
 joint_axis(j::Kinematics.Joint{Kinematics.Fixed}) = (1.0, 0.0, 0.0)
 joint_axis(j::Kinematics.Joint) = Tuple(j.jt.axis)
 
-"""HIP-side model of a Mechanism: the tree of `m` (ids as in `m`) and its current `m.angles`
-for joints that batches do not drive.  Re-create after `add_new_link`."""
+"""HIP-side model of a Mechanism.  Follows the Mechanism's state the way the reference's methods do
+(they read `m.angles` and the tree on every call, src/mechanism.jl:223-231, src/algorithm.jl:1-37):
+every batched call goes through `sync!`, which
+  * rebuilds the C model when `add_new_link` grew the tree (length(m.links) / length(m.joints)),
+  * pushes `m.angles` to kin_model_set_angles when they changed since the last push,
+and `plan!` / `coll_plan!` re-stage a cached plan whose baked angles (the joints it does NOT take as
+batch columns, `baked_angles`) differ from the current ones.  So `set_joint_angles(m, [head_pan], ...)`
+or `add_new_link` followed by a batched call sees the new state, as in the reference."""
 mutable struct HIPModel
     handle::Ptr{Cvoid}
     m::Mechanism
-    plans::Dict{Any,Ptr{Cvoid}}
+    plans::Dict{Any,Tuple{Ptr{Cvoid},Vector{Float64}}}  # request => (kin_plan, angles it baked in)
     specialize::Bool  # compile every new plan into constant-folded kernels (kin_plan_specialize)
+    angles::Vector{Float64}  # m.angles as last passed to kin_model_set_angles
+    n_links::Int             # length(m.links) the C model was built with
 end
 
-function HIPModel(m::Mechanism; specialize::Bool=true)
+function model_handle(m::Mechanism)
     J = length(m.joints)
     jt = Int32[joint_type_code(j) for j in m.joints]
     jp = Int32[j.plink_id for j in m.joints]
@@ -115,22 +123,70 @@ function HIPModel(m::Mechanism; specialize::Bool=true)
         check(ccall((:kin_model_create, libkinhip), Cint, (Ref{KinTreeDesc}, Ref{Ptr{Cvoid}}), d, h))
     end
     check(ccall((:kin_model_set_angles, libkinhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), h[], m.angles))
-    hm = HIPModel(h[], m, Dict{Any,Ptr{Cvoid}}(), specialize)
+    h[]
+end
+
+function free_plans!(hm::HIPModel)
+    for (p, _) in values(hm.plans)
+        ccall((:kin_plan_destroy, libkinhip), Cint, (Ptr{Cvoid},), p)
+    end
+    empty!(hm.plans)
+end
+
+function HIPModel(m::Mechanism; specialize::Bool=true)
+    hm = HIPModel(model_handle(m), m, Dict{Any,Tuple{Ptr{Cvoid},Vector{Float64}}}(), specialize, copy(m.angles),
+                  length(m.links))
     finalizer(hm) do x
-        for p in values(x.plans)
-            ccall((:kin_plan_destroy, libkinhip), Cint, (Ptr{Cvoid},), p)
-        end
+        free_plans!(x)
         ccall((:kin_model_destroy, libkinhip), Cint, (Ptr{Cvoid},), x.handle)
     end
     hm
 end
 
+"""Bring the C model up to the Mechanism's current tree and angles (see HIPModel)."""
+function sync!(hm::HIPModel)
+    m = hm.m
+    if length(m.links) != hm.n_links || length(m.angles) != length(hm.angles)  # add_new_link
+        free_plans!(hm)
+        ccall((:kin_model_destroy, libkinhip), Cint, (Ptr{Cvoid},), hm.handle)
+        hm.handle = model_handle(m)
+        hm.n_links = length(m.links)
+        hm.angles = copy(m.angles)
+    elseif m.angles != hm.angles  # set_joint_angle(s) since the last call
+        check(ccall((:kin_model_set_angles, libkinhip), Cint, (Ptr{Cvoid}, Ptr{Float64}), hm.handle, m.angles))
+        hm.angles = copy(m.angles)
+    end
+    hm
+end
+
+"""The angles a plan over batch joints `qj` bakes in: m.angles with the batch joints zeroed."""
+function baked_angles(m::Mechanism, qj::Vector{Int32})
+    a = copy(m.angles)
+    a[qj] .= 0.0
+    a
+end
+
 dtype_code(::Type{Float32}) = KIN_F32
 dtype_code(::Type{Float64}) = KIN_F64
 
+"""Cached plan for a request, re-staged when the angles it baked in changed (after sync!)."""
+function cached_plan!(make, hm::HIPModel, key, qj::Vector{Int32})
+    sync!(hm)
+    baked = baked_angles(hm.m, qj)
+    hit = get(hm.plans, key, nothing)
+    if hit !== nothing
+        hit[2] == baked && return hit[1]
+        ccall((:kin_plan_destroy, libkinhip), Cint, (Ptr{Cvoid},), hit[1])
+        delete!(hm.plans, key)
+    end
+    p = make()
+    hm.plans[key] = (p, baked)
+    p
+end
+
 function plan!(hm::HIPModel, ::Type{T}, qj, outs, jl, jj, flags) where {T}
     key = (T, qj, outs, jl, jj, flags)
-    get!(hm.plans, key) do
+    cached_plan!(hm, key, qj) do
         h = Ref{Ptr{Cvoid}}(C_NULL)
         GC.@preserve qj outs jj begin
             d = KinPlanDesc(dtype_code(T), length(qj), pointer(qj), length(outs), pointer(outs), jl, length(jj),
@@ -290,7 +346,7 @@ function coll_plan!(hm::HIPModel, ::Type{T}, sscc::Kinematics.SweptSphereCollisi
     ids = Int32[j.id for j in joints]
     sph = Int32[l.id for l in sscc.sphere_links]
     key = (:coll, T, ids, sph)
-    get!(hm.plans, key) do
+    cached_plan!(hm, key, ids) do
         h = Ref{Ptr{Cvoid}}(C_NULL)
         r = Float64.(sscc.sphere_radii)
         GC.@preserve ids sph r begin
@@ -348,6 +404,6 @@ function pose_const!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot
     vals, jac
 end
 
-export HIPModel, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
+export HIPModel, sync!, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
 
 end # module

@@ -20,7 +20,8 @@ import numpy as np
 import torch
 
 from . import _lib as K
-from .mechanism import Link, Mechanism, _device, _i32, _ld_of, _p, _same_device, get_transform
+from .mechanism import (Link, Mechanism, _current_device_index, _device, _i32, _ld_of, _p, _plan_device, _same_device,
+                        get_transform)
 
 _DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
 _uid = itertools.count()
@@ -60,6 +61,7 @@ class UnionSDF:
         W = np.ascontiguousarray(np.array([b.width for b in sdfs], np.float64).reshape(-1))
         self._h = C.c_void_p()
         K.check(K.lib().kin_sdf_create_boxes(len(sdfs), _p(P), _p(W), C.byref(self._h)))
+        self.device_index = _current_device_index()
 
     def __del__(self):
         if getattr(self, "_h", None) and K._lib is not None:
@@ -105,6 +107,7 @@ class CollisionPlan:
                        _p(self._r).value)
         self._h = C.c_void_p()
         K.check(K.lib().kin_coll_plan_create(m._model, C.byref(d), C.byref(self._h)))
+        self.device_index = _current_device_index()
 
     def __del__(self):
         if getattr(self, "_h", None) and K._lib is not None:
@@ -130,6 +133,8 @@ class CollisionPlan:
                 not Qt.is_contiguous():
             raise ValueError(f"Qt must be a contiguous CUDA {self.dtype} tensor of shape (ntiles, {self.n_dof}, tile)")
         nt, _, tile = Qt.shape
+        _plan_device(self, Qt)
+        _plan_device(sdf, Qt)
         dev = Qt.device
         D = torch.empty((nt, self.n_sph, tile), dtype=self.dtype, device=dev) if dists else None
         G = torch.empty((nt, self.n_sph, self.n_dof, tile), dtype=self.dtype, device=dev) if grads else None
@@ -148,6 +153,8 @@ class CollisionPlan:
         if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
         N = Q.shape[1]
+        _plan_device(self, Q)
+        _plan_device(sdf, Q)
         dev = Q.device
         D = dists if isinstance(dists, torch.Tensor) else (
             torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None)

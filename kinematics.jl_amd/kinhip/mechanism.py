@@ -247,6 +247,7 @@ class Plan:
         K.check(K.lib().kin_plan_shape(self._h, C.byref(nq), C.byref(rows), C.byref(cols)))
         self.n_qcols, self.jac_rows, self.jac_cols = nq.value, rows.value, cols.value
         self.n_out = self._o.size
+        self.device_index = _current_device_index()  # the HIP device the plan was staged on
 
     def __del__(self):
         if getattr(self, "_h", None) and K._lib is not None:
@@ -270,6 +271,7 @@ class Plan:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_qcols}, N)")
         if Q.stride(1) != 1:
             raise ValueError("Q must be configuration-contiguous (stride(1) == 1)")
+        _plan_device(self, Q)
         return Q.shape[1]
 
     def run(self, Q: torch.Tensor, poses: Optional[torch.Tensor] = None, jac: Optional[torch.Tensor] = None,
@@ -304,6 +306,7 @@ class Plan:
         nt, _, tile = Qt.shape
         if Qt.stride(2) != 1 or not 0 <= n <= nt * tile:
             raise ValueError("Qt must be configuration-contiguous and hold n configurations")
+        _plan_device(self, Qt)
         dev = Qt.device
         if poses is None and self.n_out:
             poses = torch.empty((nt, self.n_out, 12, tile), dtype=self.dtype, device=dev)
@@ -510,6 +513,21 @@ def _same_device(t: torch.Tensor, ref: torch.Tensor, what: str):
         raise ValueError(f"{what} must be a CUDA tensor on {ref.device} (got {t.device})")
 
 
+def _current_device_index() -> int:
+    try:
+        return torch.cuda.current_device()
+    except (RuntimeError, AssertionError):  # no HIP device: plan creation has failed before this
+        return -1
+
+
+def _plan_device(plan, Q: torch.Tensor):
+    """A plan's program (and its specialised code) lives on the device it was staged on.  The C-ABI
+    checks the *current* device; this checks the tensors too: Q on another device than the plan
+    would launch the plan's module on Q's stream with pointers of another GPU (a GPU fault)."""
+    if Q.device.index != plan.device_index:
+        raise ValueError(f"the plan lives on cuda:{plan.device_index} but the tensors are on {Q.device}")
+
+
 def _ld_of(t: torch.Tensor, shape, dtype) -> int:
     """Leading dimension of a [a][b][ld] SoA output given as a (possibly row-padded) view of shape
     `shape` = (a, b, N): configuration stride 1, rows `ld` apart (the C-ABI's ldp / ldj)."""
@@ -628,14 +646,25 @@ def _raise_like_julia(rc):
         raise K.error_class(rc)(msg) if rc in (K.KIN_E_KEY, K.KIN_E_METHOD) else K.KinError(rc, msg)
 
 
-def _cached_plan(m: Mechanism, key, make):
+_SINGLE_PLAN_CAP = 16
+
+
+def _cached_plan(m: Mechanism, key, make, joints=()):
     """Per-mechanism cache of the single-configuration convenience plans, keyed by the request, the
-    mechanism state they were staged with (angles of non-batched joints, tree size) and the device."""
-    key = key + (m.angles.tobytes(), len(m.joints), torch.cuda.current_device())
+    mechanism state they bake in -- the angles of the joints the plan does NOT take as batch columns
+    (the batched ones come in through Q) and the tree size -- and the device.  Least recently used
+    plans beyond _SINGLE_PLAN_CAP are dropped, so a loop of IK calls that moves the batched joints
+    reuses one plan and a loop that moves other joints does not grow device memory without bound."""
+    batched = np.zeros(len(m.angles), bool)
+    batched[[j.id - 1 for j in joints]] = True
+    key = key + (np.where(batched, 0.0, m.angles).tobytes(), len(m.joints), torch.cuda.current_device())
     plans = m.__dict__.setdefault("_single_plans", {})
-    p = plans.get(key)
+    p = plans.pop(key, None)
     if p is None:
-        p = plans[key] = make()
+        p = make()
+    plans[key] = p  # most recently used last
+    while len(plans) > _SINGLE_PLAN_CAP:
+        plans.pop(next(iter(plans)))
     return p
 
 
@@ -675,7 +704,8 @@ def point_inverse_kinematics_nakamura(m: Mechanism, link: Link, joints, point_de
     dev = _device()
     m._sync_angles()
     plan = _cached_plan(m, ("nakamura", link.id, tuple(j.id for j in joints)),
-                        lambda: m.plan(joints, jac_link=link, jac_joints=joints, with_rot=False, dtype=torch.float64))
+                        lambda: m.plan(joints, jac_link=link, jac_joints=joints, with_rot=False, dtype=torch.float64),
+                        joints)
     Q = torch.tensor([m.angles[j.id - 1] for j in joints], dtype=torch.float64, device=dev).reshape(-1, 1)
     pts = torch.tensor(np.asarray(point_desired, np.float64), device=dev).reshape(3, 1).contiguous()
     plan.point_ik_nakamura(pts, Q)
@@ -714,7 +744,7 @@ def _dls_ik_ftol(m: Mechanism, link: Link, joints, target_pose, ftol, with_rot, 
     m._sync_angles()
     plan = _cached_plan(m, ("ik", link.id, tuple(j.id for j in joints)),
                         lambda: m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=True,
-                                       dtype=torch.float64))
+                                       dtype=torch.float64), joints)
     Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
     T = np.asarray(target_pose, np.float64)
     tgt = torch.tensor(T[:3, :4].T.reshape(12), device=dev).reshape(12, 1).contiguous()

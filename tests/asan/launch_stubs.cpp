@@ -15,6 +15,8 @@ hipError_t launch_ik_dls(const KProg<T>&, const KStep<T>*, const LaunchGeom&, co
                          hipStream_t) {
     return hipErrorNoDevice;
 }
+bool ik_wants_two_phase(const IkArgs&, int64_t, int64_t) { return false; }
+bool ik_last_call_partial() { return false; }
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, T*, int64_t,
                            int64_t, const JitFns*, hipStream_t) {

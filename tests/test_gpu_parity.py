@@ -544,6 +544,84 @@ def test_ik_dls_two_phase_graph_replay(dev):
             assert torch.equal(e[0], ref[0]) and torch.equal(e[1], ref[1]), rep
 
 
+def test_ik_dls_capture_first_call(dev):
+    """a plan's first call that does not run the two-phase schedule (lanes = 4 with
+    restarts, or a one-round batch) allocates nothing, so it may be the first call inside a stream
+    capture; a first two-phase call inside a capture is refused with a message (it must allocate);
+    several graphs of one plan each own a scratch set and replay the eager results bit for bit."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+    plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    N = 1 << 16
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=93,
+                                dtype=torch.float32, device=dev)
+    T = plan.run(Qt)[0][0].contiguous()
+    torch.cuda.synchronize()
+    kw = dict(max_iters=64, restarts=3, seed=9, lam=1e-2, max_step=0.5)
+    Q0 = torch.zeros((8, N), dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        # first call of the plan, inside a capture, one-phase (lanes = 4): no allocation
+        Qa = Q0.clone()
+        ga = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, stream=s):
+            outa = plan.ik_dls(T, Qa, stream=s, lanes=4, **kw)
+        ga.replay()
+        s.synchronize()
+        refa = plan.ik_dls(T, Q0.clone(), stream=s, lanes=4, **kw)
+        s.synchronize()
+        assert torch.equal(outa[0], refa[0]) and torch.equal(outa[1], refa[1])
+        # first two-phase call inside a capture: refused (it would allocate the scratch)
+        gb = torch.cuda.CUDAGraph()
+        with pytest.raises(kinhip.KinError, match="capture"):
+            with torch.cuda.graph(gb, stream=s):
+                plan.ik_dls(T, Q0.clone(), stream=s, **kw)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        ref = [t.clone() for t in plan.ik_dls(T, Q0.clone(), stream=s, **kw)]  # eager: allocates
+        s.synchronize()
+        graphs = []
+        for k in range(6):  # 4 graphs own a set each, the 5th and 6th run one phase
+            Qg = Q0.clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                out = plan.ik_dls(T, Qg, stream=s, **kw)
+            graphs.append((g, out))
+        for rep in range(2):
+            for g, out in graphs:
+                g.replay()
+            e = plan.ik_dls(T, Q0.clone(), stream=s, **kw)
+            s.synchronize()
+            for g, out in graphs:
+                assert all(torch.equal(a, b) for a, b in zip(out, ref)), rep
+            assert all(torch.equal(a, b) for a, b in zip(e, ref)), rep
+
+
+def test_plan_refuses_tensors_of_another_device(dev):
+    """the Python mirror compares the tensors' device with the plan's (the C check only
+    sees the current device)."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+    Q = torch.zeros((8, 64), dtype=torch.float32, device=dev)
+    plan.run(Q)
+    plan.device_index = dev.index + 1  # as if staged on another GPU
+    with pytest.raises(ValueError, match="lives on"):
+        plan.run(Q)
+    with pytest.raises(ValueError, match="lives on"):
+        plan.ik_dls(torch.zeros((12, 64), dtype=torch.float32, device=dev), Q)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(np.eye(4), (0.1, 0.1, 0.1))])
+    cp = sscc.plan(arm, dtype=torch.float32)
+    cp.run(sdf, Q)
+    sdf.device_index = dev.index + 1
+    with pytest.raises(ValueError, match="lives on"):
+        cp.run(sdf, Q)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_ik_dls_two_phase_large_identical(dev, dtype):
     """A batch of more than two rounds of resident waves (2^19 targets): phase 1 may run on wave-local

@@ -121,3 +121,47 @@ def test_julia_struct_mirrors_c_struct(jl_name):
     assert [n for n, _ in jf] == [n for n, _ in cf], (jl_name, jf, cf)
     for (n, t), (_, cc) in zip(jf, cf):
         assert jl_class(t) == cc, (jl_name, n, t, cc)
+
+
+RUN_ENTRIES = ("kin_plan_run", "kin_plan_run_tiled", "kin_ik_dls_batch", "kin_ik_dls_batch_from",
+               "kin_point_ik_nakamura_batch", "kin_coll_batch", "kin_ineq_const_batch", "kin_pose_const_batch")
+
+
+def jl_functions(src):
+    """{name: body} of every top-level `function ... end` (the shim indents bodies by 4)."""
+    out = {}
+    for m in re.finditer(r"^function ([\w.!]+)\((.*?)^end\b", src, flags=re.S | re.M):
+        out.setdefault(m.group(1), []).append(m.group(2))
+    return out
+
+
+def test_every_cached_plan_path_goes_through_the_staleness_check():
+    """VERDICT r02 #1 / reference semantics (src/mechanism.jl:223-231, src/algorithm.jl:1-37: every call
+    reads the Mechanism's current angles and tree): every shim function that runs a plan gets it from
+    plan! / coll_plan!, both of which go through cached_plan!, which calls sync! (model vs m.angles /
+    the tree) before it compares the plan's baked angles; nothing else touches the plan cache."""
+    src = open(SHIM).read()
+    fns = jl_functions(src)
+    runners = 0
+    for name, bodies in fns.items():
+        for body in bodies:
+            for entry in RUN_ENTRIES:
+                if re.search(r"ccall\(\(:%s,\s*libkinhip\)" % entry, body):
+                    runners += 1
+                    assert re.search(r"\b(plan!|coll_plan!)\(hm,", body), (name, entry)
+    assert runners >= 9
+    for name in ("plan!", "coll_plan!"):
+        (body,) = fns[name]
+        assert "cached_plan!(hm, key," in body, name
+        assert "kin_plan_create" in body or "kin_coll_plan_create" in body
+    (cp,) = fns["cached_plan!"]
+    assert cp.index("sync!(hm)") < cp.index("baked_angles(") < cp.index("hit[2] == baked")
+    assert "kin_plan_destroy" in cp  # a stale plan is dropped, not reused
+    (sy,) = fns["sync!"]
+    assert "length(m.links) != hm.n_links" in sy and "kin_model_set_angles" in sy and "model_handle(m)" in sy
+    # the plan cache is only touched by cached_plan! and free_plans!
+    for name, bodies in fns.items():
+        if name in ("cached_plan!", "free_plans!", "HIPModel"):
+            continue
+        for body in bodies:
+            assert "hm.plans" not in body and "x.plans" not in body, name
