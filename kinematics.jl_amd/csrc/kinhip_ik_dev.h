@@ -210,6 +210,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << (grp * G));
 
     T Rt[9], pt[3], b0[3], qs[MAXA], b[3];
+    uint32_t blk = 0;  // active set: joints held out of the solve (bit s = phase-A step s)
     int att = 0, it = 0, res_att = INT_MAX;
     bool done = true, final_lane = false;
     uint32_t off = 0;
@@ -232,6 +233,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         final_lane = false;
         it = att > 0 ? att * L + 1 : 0;
         ep = er = T(0);
+        blk = 0;
         ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
     };
     T ro[MAXA][3], rz[MAXA][3];
@@ -312,6 +314,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 it = att * L + 1;
                 ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
                 b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
+                blk = 0;
             }
             continue;
         }
@@ -328,10 +331,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             Jb[2][1] = Lf.t[0] - b[0];
             if constexpr (ROWS == 6) Jb[2][5] = T(1);
         }
-        // pass 0: every joint; pass 1 (lanes that need it): joints sitting on a
-        // limit that the step pushes further out get weight 0 and the system is
-        // re-solved (same rule as the oracle's or_ik_dls_batch)
-        // linear Jacobian rows z x (p - o) once per iteration (both passes and dq reuse them)
+        // linear Jacobian rows z x (p - o) once per iteration (the solve and dq reuse them)
 #pragma unroll
         for (int s = 0; s < MAXA; ++s) {
             const T dx = Lf.t[0] - ro[s][0], dy = Lf.t[1] - ro[s][1], dz = Lf.t[2] - ro[s][2];
@@ -339,13 +339,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             ro[s][1] = fma(rz[s][2], dx, -(rz[s][0] * dz));
             ro[s][2] = fma(rz[s][0], dy, -(rz[s][1] * dx));
         }
-        T w[MAXA];
-#pragma unroll
-        for (int s = 0; s < MAXA; ++s) w[s] = T(1);
+        // Active set (same rule as the oracle's or_ik_dls_batch): a joint that sits on a limit and
+        // that the previous iteration's unconstrained direction pushed further out is held out of
+        // this solve (weight 0); it rejoins once the direction J_s^T y points back inside.  One
+        // solve per iteration: the set lags one iteration instead of re-solving in the same one
+        // (the re-solve ran in ~half of all lane-iterations, i.e. in nearly every wave-iteration).
         T dq[MAXA], db[3] = {T(0), T(0), T(0)};
         T mx = T(0);
-#pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {  // unrolled: pass 0 has w == 1 as a constant
+        {
             // A = J W J^T + lambda^2 I  (lower triangle)
             T A[ROWS][ROWS];
 #pragma unroll
@@ -356,8 +357,11 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
                 jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
+                if ((S[s].flags & SF_REC) && S[s].qcol >= 0) {  // (a constant in specialised kernels)
+                    const T ws = (blk >> s) & 1u ? T(0) : T(1);
 #pragma unroll
-                for (int r = 0; r < ROWS; ++r) J[r] *= w[s];
+                    for (int r = 0; r < ROWS; ++r) J[r] *= ws;
+                }
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
 #pragma unroll
@@ -415,8 +419,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 if constexpr (fast) y[r] = sm * ip[r];
                 else y[r] = sm / A[r][r];
             }
-            bool blocked = false;
-            mx = T(0);
+            uint32_t nb = 0;
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
@@ -424,14 +427,12 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 T v = T(0);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
-                v *= w[s];
-                dq[s] = v;
-                if ((qs[s] <= S[s].lo && v < T(0)) || (qs[s] >= S[s].hi && v > T(0))) {
-                    blocked = true;
-                    w[s] = T(0);
-                }
-                mx = fmax(mx, fabs(v));
+                const bool held = (blk >> s) & 1u;
+                dq[s] = held ? T(0) : v;
+                if ((qs[s] <= S[s].lo && v < T(0)) || (qs[s] >= S[s].hi && v > T(0))) nb |= 1u << s;
+                mx = fmax(mx, fabs(dq[s]));
             }
+            blk = nb;
             if (base) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
@@ -442,7 +443,6 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                     mx = fmax(mx, fabs(v));
                 }
             }
-            if (!blocked) break;
         }
         const T sc = mx > a.max_step ? a.max_step / mx : T(1);
 #pragma unroll

@@ -665,6 +665,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
         or_mech* m = or_mech_clone(proto);
         double* a = (double*)malloc(sizeof(double) * (ndof + 1));
         double* J = (double*)malloc(sizeof(double) * 6 * (ndof + 1));
+        double* Jw = (double*)malloc(sizeof(double) * 6 * (ndof + 1));
         double* lo = (double*)malloc(sizeof(double) * (ndof + 1));
         double* hi = (double*)malloc(sizeof(double) * (ndof + 1));
         for (int32_t c = 0; c < ndof; ++c) { /* joints that cannot move the link are left untouched */
@@ -681,7 +682,8 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
             double ep = 0, er = 0;
             const int32_t attempt_len = prm->restarts > 0 ? prm->max_iters / (prm->restarts + 1) : 0;
             double a0[64];
-            for (int32_t c = 0; c < ndof; ++c) a0[c] = a[c];
+            int held[64];
+            for (int32_t c = 0; c < ndof; ++c) { a0[c] = a[c]; held[c] = 0; }
             for (;; ++it) {
                 or_set_joint_angles(m, n_q, qids, a);
                 tf_t now = get_transform(m, link_id);
@@ -702,37 +704,35 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                         } else {
                             a[c] = a0[c];
                         }
+                        held[c] = 0;
                     }
                     continue;
                 }
                 memset(J, 0, sizeof(double) * 6 * ndof);
                 or_get_jacobian(m, link_id, n_q, qids, prm->with_rot, 0, J);
                 double dq[64], mx = 0;
-                /* pass 0: all joints; pass 1 (only if needed): joints sitting on a
-                 * limit that the step pushes further out are dropped (columns zeroed) */
-                for (int pass = 0; pass < 2; ++pass) {
+                /* active set: joints held[k] (on a limit, pushed further out by the previous
+                 * iteration's direction) are dropped from this solve (columns zeroed); every joint's
+                 * unconstrained direction J_k^T y decides the set of the next iteration */
+                {
                     double A[36], y[6];
                     for (int r = 0; r < rows; ++r) y[r] = e[r];
+                    for (int32_t k = 0; k < ndof; ++k)
+                        for (int r = 0; r < rows; ++r) Jw[r + rows * k] = held[k] ? 0.0 : J[r + rows * k];
                     for (int c = 0; c < rows; ++c)
                         for (int r = 0; r < rows; ++r) {
                             double s = 0;
-                            for (int32_t k = 0; k < ndof; ++k) s += J[r + rows * k] * J[c + rows * k];
+                            for (int32_t k = 0; k < ndof; ++k) s += Jw[r + rows * k] * Jw[c + rows * k];
                             A[r + rows * c] = s + (r == c ? prm->lambda * prm->lambda : 0.0);
                         }
                     chol_solve(A, rows, y);
-                    int blocked = 0;
-                    mx = 0;
                     for (int32_t k = 0; k < ndof; ++k) {
                         double s = 0;
                         for (int r = 0; r < rows; ++r) s += J[r + rows * k] * y[r];
-                        dq[k] = s;
-                        if ((a[k] <= lo[k] && s < 0) || (a[k] >= hi[k] && s > 0)) {
-                            blocked = 1;
-                            for (int r = 0; r < rows; ++r) J[r + rows * k] = 0.0;
-                        }
-                        if (fabs(s) > mx) mx = fabs(s);
+                        dq[k] = held[k] ? 0.0 : s;
+                        held[k] = (a[k] <= lo[k] && s < 0) || (a[k] >= hi[k] && s > 0);
+                        if (fabs(dq[k]) > mx) mx = fabs(dq[k]);
                     }
-                    if (!blocked) break;
                 }
                 double sc = mx > prm->max_step ? prm->max_step / mx : 1.0;
                 for (int32_t k = 0; k < ndof; ++k) {
@@ -745,7 +745,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
             if (iters_out) iters_out[i] = it;
             if (err_out) { err_out[i] = ep; err_out[n + i] = er; }
         }
-        free(a); free(J); free(lo); free(hi);
+        free(a); free(J); free(Jw); free(lo); free(hi);
         or_mech_destroy(m);
     }
 }

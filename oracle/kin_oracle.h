@@ -100,7 +100,10 @@ void or_point_ik_nakamura_batch(const or_mech* proto, int64_t n, double* q, int6
 /* ---- build-defined damped-least-squares IK (config 4), restated for parity ----
  * Not a reference algorithm (the reference uses NLopt SLSQP, parity unpinned);
  * this is the CPU statement of the GPU kernel's algorithm so the kernel's
- * iterates can be checked.  See DESIGN.md "ik_dls". */
+ * iterates can be checked.  See DESIGN.md "ik_dls".  Per iteration: e = [p* - p; log(R* R^T)],
+ * dq = W J^T (J W J^T + lambda^2 I)^-1 e with W = diag(joint not held), |dq|_inf clamped to
+ * max_step, q clamped to the limits; a joint is held in the next iteration when it sits on a limit
+ * and J_k^T (...)^-1 e of this one pushes it further out (active set, one iteration behind). */
 typedef struct {
     int32_t max_iters;
     double lambda;     /* damping */

@@ -567,7 +567,8 @@ def test_ik_dls_capture_first_call(dev):
         Qa = Q0.clone()
         ga = torch.cuda.CUDAGraph()
         with torch.cuda.graph(ga, stream=s):
-            outa = plan.ik_dls(T, Qa, stream=s, lanes=4, **kw)
+            outa = plan.ik_dls(T, Qa, stream=s, lanes=4, Q0=Q0, **kw)
+        ga.replay()
         ga.replay()
         s.synchronize()
         refa = plan.ik_dls(T, Q0.clone(), stream=s, lanes=4, **kw)
@@ -587,7 +588,7 @@ def test_ik_dls_capture_first_call(dev):
             Qg = Q0.clone()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
-                out = plan.ik_dls(T, Qg, stream=s, **kw)
+                out = plan.ik_dls(T, Qg, stream=s, Q0=Q0, **kw)  # seeds read from Q0: replays repeat
             graphs.append((g, out))
         for rep in range(2):
             for g, out in graphs:
