@@ -245,7 +245,11 @@ typedef struct kin_ik_params {
     double tol_pos;     /* |dp| tolerance, e.g. 1e-3 */
     double tol_rot;     /* |axis-angle error| tolerance, e.g. 1e-3 */
     double max_step;    /* max |dq|_inf per iteration, e.g. 0.5 */
-    int32_t with_rot;   /* 0: position only */
+    int32_t with_rot;   /* 0: position only; 1: residual [p* - p; log(R* R^T)] (axis-angle) with the geometric
+                           Jacobian; 2: the reference's f_objective (src/inverse_kinematics.jl:38-50): residual
+                           [p* - p; rpy(target) - rpy(pose)] (angle differences wrapped to (-pi, pi]) with the
+                           rpy_jac=true Jacobian, converged when |dp| < tol_pos and |d rpy| < tol_rot (err row 1
+                           is then |d rpy|) */
     int32_t restarts;   /* 0: none; else max_iters is split into restarts+1 attempts and each new
                            attempt re-draws the relevant joints uniformly within their limits
                            (U[-pi, pi] if unbounded) from a counter hash of (seed, i, attempt, column) */

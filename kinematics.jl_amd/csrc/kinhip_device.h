@@ -319,6 +319,32 @@ __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T 
     }
 }
 
+// rpy(tf) (src/transform.jl:45-48: RotZYX angles as [roll, pitch, yaw]) of a row-major rotation,
+// and the rpy_derivative! coefficients at it (src/algorithm.jl:56-63, a = -rpy):
+//   d(rpy)/dt = [k0 x + k1 y, k2 x + k3 y, k4 x + k5 y + z] for an angular velocity (x, y, z)
+template <typename T>
+__device__ __forceinline__ void rpy_and_rate(const T (&r)[9], T (&rpy)[3], T (&k)[6]) {
+    const T t1 = atan2_t(r[3], r[0]);
+    T s1, c1;
+    sincos_t(t1, &s1, &c1);
+    const T t2 = atan2_t(-r[6], fma(r[3], s1, r[0] * c1));
+    const T t3 = atan2_t(fma(r[2], s1, -(r[5] * c1)), fma(r[4], c1, -(r[1] * s1)));
+    rpy[0] = t3; rpy[1] = t2; rpy[2] = t1;
+    T s2, c2;
+    sincos_t(t2, &s2, &c2);  // a2 = -t2: cos(a2) = c2, sin(a2) = -s2; a3 = -t1: cos = c1, sin = -s1
+    const T ic2 = T(1) / c2;
+    k[0] = c1 * ic2; k[1] = s1 * ic2;
+    k[2] = -s1; k[3] = c1;
+    k[4] = c1 * s2 * ic2; k[5] = s1 * s2 * ic2;
+}
+
+// angle difference wrapped to (-pi, pi]
+template <typename T>
+__device__ __forceinline__ T wrap_pi(T d) {
+    const T tp = T(6.283185307179586476925286766559);
+    return d - tp * rint(d * T(0.15915494309189533576888376337251));
+}
+
 template <typename T>
 __device__ __forceinline__ void base_frame(Fr<T>& f, T bx, T by, T th) {  // src/transform.jl:33-37
     set_identity(f);

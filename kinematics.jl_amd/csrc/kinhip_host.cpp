@@ -1385,6 +1385,8 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     if (const int rc = check_device(p->device, "kin_ik_dls_batch", "the plan")) return rc;
     if (prm->max_iters < 0 || !(prm->lambda >= 0) || !(prm->max_step > 0) || prm->restarts < 0)
         return set_error(KIN_E_INVALID, "bad IK parameters");
+    if (prm->with_rot < 0 || prm->with_rot > 2)
+        return set_error(KIN_E_INVALID, "kin_ik_params.with_rot must be 0, 1 or 2 (reference rpy objective)");
     if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
         return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
     if (prm->index_base < 0) return set_error(KIN_E_INVALID, "kin_ik_params.index_base < 0");

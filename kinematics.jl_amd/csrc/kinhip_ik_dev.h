@@ -132,6 +132,10 @@ struct IkArgsT {
     // starting angles (kin_ik_dls_batch_from): read from q0 (same leading dimension as q) instead of
     // q, so q is written without being read and a caller keeps q0 for the next batch; null: q in place
     const T* q0;
+    // 1: the reference's objective (kin_ik_params.with_rot = 2, src/inverse_kinematics.jl:38-50):
+    // residual [p* - p; rpy* - rpy] (angle differences wrapped to (-pi, pi]) with the rpy_jac=true
+    // Jacobian rows, converged on |dp| < tol_pos and |d rpy| < tol_rot; 0: the axis-angle residual
+    int32_t rpy_obj;
 };
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
@@ -210,6 +214,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const uint64_t gmask = (G == 64) ? ~0ull : (((1ull << G) - 1ull) << (grp * G));
 
     T Rt[9], pt[3], b0[3], qs[MAXA], b[3];
+    T trpy[3] = {T(0), T(0), T(0)};  // rpy of the target (reference objective)
     uint32_t blk = 0;  // active set: joints held out of the solve (bit s = phase-A step s)
     int att = 0, it = 0, res_att = INT_MAX;
     bool done = true, final_lane = false;
@@ -222,6 +227,10 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
             for (int c = 0; c < 3; ++c) Rt[3 * r + c] = KIN_IK_LD(tgt, r + 3 * c, ldt, off);
             pt[r] = KIN_IK_LD(tgt, 9 + r, ldt, off);
+        }
+        if (ROWS == 6 && a.rpy_obj) {
+            T kk[6];
+            rpy_and_rate(Rt, trpy, kk);
         }
         b0[0] = b0[1] = b0[2] = T(0);
         if (base)
@@ -289,9 +298,17 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
         ep = sqrt_fast(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
         er = T(0);
+        T kr[6];  // rpy_derivative! coefficients (reference objective)
         if constexpr (ROWS == 6) {
             T w[3];
-            rot_error(Rt, Lf.r, w);
+            if (a.rpy_obj) {  // wave-uniform
+                T r[3];
+                rpy_and_rate(Lf.r, r, kr);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) w[k] = wrap_pi(trpy[k] - r[k]);
+            } else {
+                rot_error(Rt, Lf.r, w);
+            }
             e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
             er = sqrt_fast(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
@@ -338,6 +355,18 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             ro[s][0] = fma(rz[s][1], dz, -(rz[s][2] * dy));
             ro[s][1] = fma(rz[s][2], dx, -(rz[s][0] * dz));
             ro[s][2] = fma(rz[s][0], dy, -(rz[s][1] * dx));
+        }
+        if constexpr (ROWS == 6) {
+            if (a.rpy_obj) {  // angular rows -> d(rpy)/dq (get_jacobian!(...; rpy_jac=true))
+#pragma unroll
+                for (int s = 0; s < MAXA; ++s) {
+                    if (S[s].jkind == MOT_PRISM) continue;  // [z; 0]: its linear part is z itself
+                    const T x = rz[s][0], y = rz[s][1], z = rz[s][2];
+                    rz[s][0] = fma(kr[0], x, kr[1] * y);
+                    rz[s][1] = fma(kr[2], x, kr[3] * y);
+                    rz[s][2] = fma(kr[4], x, fma(kr[5], y, z));
+                }
+            }
         }
         // Active set (same rule as the oracle's or_ik_dls_batch): a joint that sits on a limit and
         // that the previous iteration's unconstrained direction pushed further out is held out of

@@ -258,16 +258,20 @@ function Kinematics.get_jacobian(hm::HIPModel, link::Link, joints::Vector{<:Join
 end
 
 """Batched IK (damped least squares on the GPU): targets (N, 12) 3x4 poses, Q (N, dof) seeds, solved in place.
-Returns (Q, iters, err); converged where iters <= max_iters (max_iters + 1: no attempt converged)."""
+Returns (Q, iters, err); converged where iters <= max_iters (max_iters + 1: no attempt converged).
+`rpy_objective=true` solves the reference's own objective (f_objective, src/inverse_kinematics.jl:38-50:
+[p* - p; rpy* - rpy] with the rpy_jac Jacobian; tol_rot then bounds |d rpy|)."""
 function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
                                         Q::ROCMatrix{T}; max_iters=64, lambda=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-                                        max_step=0.5, with_rot=true, restarts=0, seed=0, lanes=0, index_base=0) where {T}
+                                        max_step=0.5, with_rot=true, rpy_objective=false, restarts=0, seed=0, lanes=0,
+                                        index_base=0) where {T}
     N = size(Q, 1)
     ids = Int32[j.id for j in joints]
     p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
     iters = ROCVector{Int32}(undef, N)
     err = ROCMatrix{T}(undef, N, 2)
-    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, with_rot, restarts, seed, lanes, index_base)
+    mode = with_rot ? (rpy_objective ? 2 : 1) : 0
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, mode, restarts, seed, lanes, index_base)
     check(ccall((:kin_ik_dls_batch, libkinhip), Cint,
                 (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64,
                  Ptr{Cvoid}),

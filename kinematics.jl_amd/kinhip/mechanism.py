@@ -343,7 +343,10 @@ class Plan:
         set sharded over ranks solves exactly as in one process.  iters > max_iters: not converged.
         `Q0`: starting angles read from Q0 (same shape and strides as Q, not modified) and Q written
         without being read (``kin_ik_dls_batch_from``): the results of ``Q.copy_(Q0)`` + the in-place
-        call, without the copy."""
+        call, without the copy.
+        `with_rot`: 0 position only, 1 (True) axis-angle residual, 2 the reference's objective
+        (src/inverse_kinematics.jl:38-50: [p* - p; rpy* - rpy] with the rpy_jac Jacobian; `tol_rot`
+        then bounds |d rpy| and err[1] is |d rpy|)."""
         N = self._check_q(Q)
         if Q0 is not None:
             _same_device(Q0, Q, "Q0")

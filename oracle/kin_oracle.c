@@ -689,7 +689,17 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                 tf_t now = get_transform(m, link_id);
                 double e[6];
                 for (int k = 0; k < 3; ++k) e[k] = M(tgt, k, 3) - M(now, k, 3);
-                if (prm->with_rot) rot_error(&tgt, &now, e + 3);
+                if (prm->with_rot == 2) { /* the reference's f_objective (src/inverse_kinematics.jl:38-50) */
+                    double rt[3], rn[3];
+                    rpy_of(&tgt, rt);
+                    rpy_of(&now, rn);
+                    for (int k = 0; k < 3; ++k) {
+                        const double d = rt[k] - rn[k]; /* wrapped to (-pi, pi] */
+                        e[3 + k] = d - 6.283185307179586476925286766559 * rint(d * 0.15915494309189533576888376337251);
+                    }
+                } else if (prm->with_rot) {
+                    rot_error(&tgt, &now, e + 3);
+                }
                 ep = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
                 er = prm->with_rot ? sqrt(e[3] * e[3] + e[4] * e[4] + e[5] * e[5]) : 0.0;
                 if ((ep < prm->tol_pos && er < prm->tol_rot) || it >= prm->max_iters) break;
@@ -709,7 +719,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                     continue;
                 }
                 memset(J, 0, sizeof(double) * 6 * ndof);
-                or_get_jacobian(m, link_id, n_q, qids, prm->with_rot, 0, J);
+                or_get_jacobian(m, link_id, n_q, qids, prm->with_rot != 0, prm->with_rot == 2, J);
                 double dq[64], mx = 0;
                 /* active set: joints held[k] (on a limit, pushed further out by the previous
                  * iteration's direction) are dropped from this solve (columns zeroed); every joint's

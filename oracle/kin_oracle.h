@@ -110,7 +110,8 @@ typedef struct {
     double tol_pos;    /* |dp| */
     double tol_rot;    /* |rotation error| (axis-angle) */
     double max_step;   /* clamp on |dq|_inf per iteration */
-    int32_t with_rot;
+    int32_t with_rot;  /* 0: position only, 1: axis-angle residual, 2: the reference's [p* - p; rpy* - rpy]
+                          residual (wrapped) with the rpy_jac Jacobian (src/inverse_kinematics.jl:38-50) */
     int32_t restarts;  /* attempts = restarts + 1, each max_iters / attempts iterations */
     uint64_t seed;     /* re-seed stream: ik_seed_u01(seed, config index, attempt, column) */
 } or_ik_params;
