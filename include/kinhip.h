@@ -199,7 +199,8 @@ enum {
     KIN_SPEC_FK = 1u,        /* kin_plan_run(_tiled), kin_pose_const_batch (not the one-shot kin_get_*_batch) */
     KIN_SPEC_IK = 2u,        /* kin_ik_dls_batch (with_rot 0/1, every lane count) */
     KIN_SPEC_NAKAMURA = 4u,  /* kin_point_ik_nakamura_batch */
-    KIN_SPEC_COLL = 8u       /* kin_coll_batch, kin_ineq_const_batch (spheres folded; boxes stay data) */
+    KIN_SPEC_COLL = 8u,      /* kin_coll_batch, kin_ineq_const_batch (spheres folded; boxes stay data) */
+    KIN_SPEC_IK_COLL = 16u   /* kin_ik_coll_batch (plans of kin_coll_ik_plan_create) */
 };
 KINHIP_API int kin_plan_specialize(kin_plan* p, uint32_t kernels);
 /* The KIN_SPEC_* mask the plan currently runs specialised. */
@@ -339,6 +340,37 @@ KINHIP_API int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, doubl
                                     const void* q, int64_t ldq, int64_t tsq, int64_t n, void* dists, int64_t ldd,
                                     int64_t tsd, void* grads, int64_t ldg, int64_t tsg, void* min_dist, int64_t tsm,
                                     void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Collision-aware IK: inverse_kinematics!(m, link, joints, target, sscc, sdf;  */
+/* use_bistage) (src/inverse_kinematics.jl:1-21), many targets per launch       */
+/* ------------------------------------------------------------------------- */
+/* An IK plan of `link_id` over the q joints (kin_ik_dls_batch works on it: stage 1 of the bistage
+ * solve) whose swept spheres are staged on the same chain (kin_coll_batch works on it too).  Every
+ * sphere must hang, through fixed or non-batched joints, off the root -> link path; chains of at most
+ * 8 steps (KIN_E_UNSUPPORTED otherwise).  Zero spheres is the plain pose problem (the reference's own
+ * PR2 test builds its checker with none, test/test_inverse_kinematics.jl:63). */
+KINHIP_API int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* desc, int32_t link_id, kin_plan** out);
+
+typedef struct kin_ik_coll_params {
+    double margin;  /* IneqConst(sscc, joints, sdf, 1, margin): every sphere at least margin from the union
+                       (the reference's stage 2 uses 0.02, src/inverse_kinematics.jl:16) */
+    double band;    /* spheres with d < margin + band get a penalty row pushing them to margin + band (e.g. 0:
+                       rows only for violating spheres; a positive band keeps a clearance) */
+    double weight;  /* weight of a sphere row against the pose rows (e.g. 1) */
+    double feas;    /* converged only when every sphere has d >= margin - feas (e.g. 1e-6) */
+} kin_ik_coll_params;
+/* Stage 2 of the bistage solve for N targets (stage 1 = kin_ik_dls_batch_from on the same plan): from
+ * q0 ([n_q(+3)][ldq], read; q0 == q is in place) damped Gauss-Newton steps on the pose residual of
+ * kin_ik_params.with_rot (2 = the reference's rpy objective) plus one-sided penalty rows
+ * a_k = grad sdf^T J_k of the spheres inside the band, normal equations over the q joints (+ base),
+ * joint limits by an active set and a clamp; restarts as in kin_ik_dls_batch (lanes ignored, lambda > 0).
+ * Converged (iters <= max_iters, else max_iters + 1) when |dp| < tol_pos, |rot| < tol_rot and every
+ * sphere has d >= margin - feas.  err: [3][lde] |dp|, |rot err|, min sphere distance (or NULL). */
+KINHIP_API int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
+                                 const kin_ik_coll_params* cprm, const void* target, int64_t ldt, const void* q0,
+                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,
+                                 void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Planning constraints over waypoints (src/planning.jl) */

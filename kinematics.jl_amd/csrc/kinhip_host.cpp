@@ -186,8 +186,10 @@ struct kin_plan {
     KProg<float> pf{};
     KProg<double> pd{};
     LaunchGeom geom{256, 0, 8};
-    // collision plans (kin_coll_plan_create)
+    // collision plans (kin_coll_plan_create); is_coll_ik: also an IK plan of the spheres' chain
+    // (kin_coll_ik_plan_create: kin_ik_dls_batch, kin_ik_coll_batch, kin_coll_batch)
     bool is_coll = false;
+    bool is_coll_ik = false;
     int32_t n_sph = 0;
     void* d_sph = nullptr;
     // spheres on several chains: one staged program per chain (kin_coll_plan_create)
@@ -312,6 +314,10 @@ struct Stager {
     const int32_t* sph_out = nullptr;  // global sphere index of each desc sphere (multi-chain plans)
     std::vector<SphD> spheres;
     int32_t sph_root0 = 0, sph_root1 = 0;
+    // a static last edge into the spine folded into Xlast (no step): the spine link and the
+    // transform from the previous chain node's canonical frame to it (spheres on the spine, k_ik_coll)
+    int32_t fold_spine = -1;
+    M34 fold_X = m_identity();
     // LDS slots
     std::vector<int> slot_of_link, slot_refs;
     std::vector<int> free_slots;
@@ -443,6 +449,10 @@ struct Stager {
             if (x < 0 || on_chain[x] < 0)
                 return set_error(KIN_E_UNSUPPORTED, "coll plan: sphere " + std::to_string(k) + " is on another tree");
             M34 S = hasX[x] ? Xinv[x] : m_identity();
+            if (x == fold_spine) {  // the spine has no step: carry the sphere by the node above it
+                S = fold_X;
+                x = chain[on_chain[x] - 1];
+            }
             for (size_t pi = path.size(); pi-- > 0;) S = m_mul(S, m.joint_tf(path[pi], m.angles[path[pi]]));
             SphD sd;
             const double c0 = coll->centers ? coll->centers[3 * k] : 0.0;
@@ -597,6 +607,8 @@ struct Stager {
                     for (size_t p = path.size(); p-- > 0;) Xl = m_mul(Xl, m.joint_tf(path[p], m.angles[path[p]]));
                     lhx = !m_is_identity(Xl);
                     spine_out = outs_of[v].empty() ? -1 : outs_of[v][0];
+                    fold_spine = v;
+                    fold_X = Xl;
                 } else if (k > 0 || !outs_of[v].empty()) {
                     edge_step[k] = (int32_t)steps.size();
                     emit_edge(v, LOAD_NONE);
@@ -1055,7 +1067,9 @@ int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
     if (!p) return set_error(KIN_E_INVALID, "kin_plan_specialize: null plan");
     if (const int rc = check_device(p->device, "kin_plan_specialize", "the plan")) return rc;
     uint32_t applies = 0;
-    if (p->is_coll) {
+    if (p->is_coll_ik) {
+        applies = KIN_SPEC_COLL | KIN_SPEC_IK | KIN_SPEC_IK_COLL;
+    } else if (p->is_coll) {
         applies = KIN_SPEC_COLL;
     } else {
         applies = KIN_SPEC_FK;
@@ -1255,6 +1269,64 @@ int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** 
     }
     top->n_sph = c->n_spheres;
     *out = top.release();
+    return KIN_OK;
+}
+
+int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* c, int32_t link_id, kin_plan** out) {
+    if (!m || !c || !out) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: null argument");
+    if (c->n_spheres < 0 || (c->n_spheres && (!c->sphere_link_ids || !c->radii)))
+        return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: spheres need link ids and radii");
+    if (c->n_q < 1 || !c->q_joint_ids) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: no q joints");
+    const int32_t out_ids[1] = {link_id};
+    // an IK plan of `link` over the q joints (get_jacobian! over them, geometric rows) whose spheres are
+    // staged on the same chain (every sphere must hang off the root -> link path)
+    kin_plan_desc d{c->dtype, c->n_q, c->q_joint_ids, 1, out_ids, link_id, c->n_q, c->q_joint_ids, KIN_WITH_ROT};
+    auto P = std::make_unique<kin_plan>();
+    Stager st(*m, d);
+    st.coll = c;
+    const int rc = st.run(*P);
+    if (rc != KIN_OK) return rc;
+    if (!P->ik_ok) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: " + P->ik_why);
+    if (P->geom.maxA > kIkcMaxChain)
+        return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: chains of more than " +
+                                                std::to_string(kIkcMaxChain) + " steps are not supported");
+    P->is_coll_ik = true;
+    *out = P.release();
+    return KIN_OK;
+}
+
+int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
+                      const void* target, int64_t ldt, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters,
+                      void* err, int64_t lde, void* stream) {
+    if (!p || !sdf || !prm || !cp) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: null argument");
+    if (!p->is_coll_ik) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: plan was not made by kin_coll_ik_plan_create");
+    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+    if (n == 0) return KIN_OK;
+    if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
+    if (const int rc = check_device(p->device, "kin_ik_coll_batch", "the plan")) return rc;
+    if (const int rc = check_device(sdf->device, "kin_ik_coll_batch", "the kin_sdf")) return rc;
+    if (prm->max_iters < 0 || !(prm->lambda > 0) || !(prm->max_step > 0) || prm->restarts < 0 ||
+        prm->with_rot < 0 || prm->with_rot > 2 || prm->index_base < 0)
+        return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad IK parameters (lambda must be > 0)");
+    if (!std::isfinite(cp->margin) || !(cp->band >= 0) || !(cp->weight > 0) || !(cp->feas >= 0))
+        return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad collision parameters");
+    const IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
+                   prm->restarts, prm->seed, 1, prm->index_base};
+    const IkcArgs c{cp->margin, cp->band, cp->weight, cp->feas};
+    const CollArgs ca{INFINITY, 0.0, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
+                      {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};
+    hipError_t e;
+    if (p->dtype == KIN_F32)
+        e = launch_ik_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
+                                  (const KBox<float>*)sdf->d_f32, p->geom, ca, c, a, (const float*)target, ldt,
+                                  (const float*)(q0 == q ? nullptr : q0), (float*)q, ldq, n, iters, (float*)err, lde,
+                                  jit_fns(p->jit), (hipStream_t)stream);
+    else
+        e = launch_ik_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
+                                   (const KBox<double>*)sdf->d_f64, p->geom, ca, c, a, (const double*)target, ldt,
+                                   (const double*)(q0 == q ? nullptr : q0), (double*)q, ldq, n, iters, (double*)err,
+                                   lde, jit_fns(p->jit), (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_coll launch: ") + hipGetErrorString(e));
     return KIN_OK;
 }
 

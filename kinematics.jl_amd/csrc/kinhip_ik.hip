@@ -1,6 +1,7 @@
 // kinhip_ik.hip -- k_ik_dls (batched DLS IK with restarts) and k_nakamura.
 // (gfx950 only; shared helpers in kinhip_device.h)
 #include "kinhip_ik_dev.h"
+#include "kinhip_ikc_dev.h"
 
 namespace kinhip {
 namespace {
@@ -24,6 +25,17 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
                                                   const T* __restrict__ pts, int64_t ldpt, T* __restrict__ q,
                                                   int64_t ldq, int64_t n) {
     nakamura_body<T, MAXA>(P, S, pts, ldpt, q, ldq, n);
+}
+
+template <typename T, int MAXA, int ROWS>
+__global__ __launch_bounds__(64) void k_ik_coll(const KProg<T> P, const KStep<T>* __restrict__ S,
+                                                const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
+                                                const CollArgs ca, const IkcArgsT<T> cz, const IkArgsT<T> a,
+                                                const T* __restrict__ tgt, int64_t ldt, T* __restrict__ q, int64_t ldq,
+                                                int64_t n, int32_t* __restrict__ iters, T* __restrict__ err,
+                                                int64_t lde) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    ikc_body<T, MAXA, ROWS>(P, S, sph, boxes, ca, cz, a, tgt, ldt, q, ldq, n, iters, err, lde, smem);
 }
 
 }  // namespace
@@ -204,6 +216,55 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     return hipSuccess;
 }
 
+// k_ik_coll: one target per lane, 64-lane workgroups (a few thousand targets still spread over
+// many CUs); the union's boxes in LDS for the argmin gathers (k_coll)
+template <typename T>
+hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                          const LaunchGeom& g, const CollArgs& ca, const IkcArgs& c, const IkArgs& a, const T* target,
+                          int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err, int64_t lde,
+                          const JitFns* jf, hipStream_t st) {
+    int L, natt;
+    ik_attempts(a, &L, &natt);
+    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
+                  0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
+    const IkcArgsT<T> cz{T(c.margin), T(c.band), T(c.weight), T(c.feas)};
+    const size_t lds = ca.n_boxes <= kCollLdsBoxes ? (size_t)ca.n_boxes * sizeof(KBox<T>) : 0;
+    for (int64_t s0 = 0; s0 < n; s0 += kIkChunk) {
+        const int64_t cn = std::min(kIkChunk, n - s0);
+        at.ibase = a.index_base + s0;
+        at.q0 = q0 ? q0 + s0 : nullptr;
+        const T* tc = target + s0;
+        T* qc = q + s0;
+        int32_t* ic = iters ? iters + s0 : iters;
+        T* ec = err ? err + s0 : err;
+        const unsigned grid = (unsigned)((cn + 63) / 64);
+        const hipFunction_t jk = jf ? jf->ikc[a.with_rot ? 1 : 0] : nullptr;
+        if (jk) {
+            int64_t cc = cn;
+            CollArgs cac = ca;
+            IkcArgsT<T> czc = cz;
+            void* args[] = {(void*)&boxes, (void*)&cac, (void*)&czc, (void*)&at, (void*)&tc, (void*)&ldt,
+                            (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&ic, (void*)&ec, (void*)&lde};
+            const hipError_t e = hipModuleLaunchKernel(jk, grid, 1, 1, 64, 1, 1, (unsigned)lds, st, args, nullptr);
+            if (e != hipSuccess) return e;
+            continue;
+        }
+#define KIN_IKC(MA, R) \
+        hipLaunchKernelGGL((k_ik_coll<T, MA, R>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, tc, ldt, qc, ldq, cn, ic, ec, lde)
+        if (g.maxA == 4) {
+            if (a.with_rot) KIN_IKC(4, 6); else KIN_IKC(4, 3);
+        } else if (g.maxA == 8) {
+            if (a.with_rot) KIN_IKC(8, 6); else KIN_IKC(8, 3);
+        } else {
+            return hipErrorNotSupported;  // (kin_coll_ik_plan_create refuses longer chains)
+        }
+#undef KIN_IKC
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,
                            int64_t ldpt, T* q, int64_t ldq, int64_t n, const JitFns* jf, hipStream_t st) {
@@ -233,7 +294,11 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
                                          const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t, \
                                          const JitFns*, const IkScratch&, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
-                                           int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);
+                                           int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);          \
+    template hipError_t launch_ik_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, \
+                                          const LaunchGeom&, const CollArgs&, const IkcArgs&, const IkArgs&,    \
+                                          const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*,       \
+                                          int64_t, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

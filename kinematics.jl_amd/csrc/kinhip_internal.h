@@ -54,6 +54,7 @@ struct JitFns {
     hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
+    hipFunction_t ikc[2] = {};    // collision-aware IK [rows == 6]
 };
 
 // jf: the plan-specialised kernels (kinhip_jit.cpp) or null for the generic one
@@ -91,6 +92,18 @@ template <typename T>
 hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const IkArgs& a,
                          const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
                          T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st);
+
+// collision-aware IK (k_ik_coll, kinhip_ikc_dev.h): sphere-distance bound and penalty rows
+struct IkcArgs {
+    double margin, band, weight, feas;
+};
+constexpr int kIkcMaxChain = 8;  // generic k_ik_coll kernels: chains of <= 8 steps
+
+template <typename T>
+hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                          const LaunchGeom& g, const CollArgs& ca, const IkcArgs& c, const IkArgs& a, const T* target,
+                          int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err, int64_t lde,
+                          const JitFns* jf, hipStream_t st);
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,

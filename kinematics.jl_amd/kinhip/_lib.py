@@ -22,7 +22,7 @@ KIN_E_UNSUPPORTED, KIN_E_NOMEM, KIN_E_PARSE, KIN_E_IO = -5, -6, -7, -8
 KIN_F32, KIN_F64 = 0, 1
 KIN_JOINT_FIXED, KIN_JOINT_REVOLUTE, KIN_JOINT_PRISMATIC = 0, 1, 2
 KIN_WITH_ROT, KIN_RPY_JAC, KIN_ZERO_FILL = 1, 2, 4
-KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_NAKAMURA, KIN_SPEC_COLL = 1, 2, 4, 8
+KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_NAKAMURA, KIN_SPEC_COLL, KIN_SPEC_IK_COLL = 1, 2, 4, 8, 16
 
 # every entry point include/kinhip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -38,6 +38,7 @@ EXPORTS = [
     "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch", "kin_coll_batch_tiled",
     "kin_ineq_const_batch", "kin_ineq_const_batch_tiled", "kin_pose_const_batch",
+    "kin_coll_ik_plan_create", "kin_ik_coll_batch",
 ]
 
 
@@ -72,6 +73,10 @@ class IkParams(C.Structure):
     _fields_ = [("max_iters", C.c_int32), ("lam", C.c_double), ("tol_pos", C.c_double),
                 ("tol_rot", C.c_double), ("max_step", C.c_double), ("with_rot", C.c_int32),
                 ("restarts", C.c_int32), ("seed", C.c_uint64), ("lanes", C.c_int32), ("index_base", C.c_int64)]
+
+
+class IkCollParams(C.Structure):
+    _fields_ = [("margin", C.c_double), ("band", C.c_double), ("weight", C.c_double), ("feas", C.c_double)]
 
 
 _lib = None
@@ -129,6 +134,8 @@ def lib():
         "kin_ineq_const_batch_tiled": ([P, P, C.c_double, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P],
                                        C.c_int),
         "kin_pose_const_batch": ([P, P, I64, P, I64, I64, P, I64, P, I64, P, I64, P], C.c_int),
+        "kin_coll_ik_plan_create": ([P, P, I32, P], C.c_int),
+        "kin_ik_coll_batch": ([P, P, P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

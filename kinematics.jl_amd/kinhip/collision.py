@@ -20,8 +20,8 @@ import numpy as np
 import torch
 
 from . import _lib as K
-from .mechanism import (Link, Mechanism, _current_device_index, _device, _i32, _ld_of, _p, _plan_device, _same_device,
-                        get_transform)
+from .mechanism import (Link, Mechanism, Plan, _current_device_index, _device, _i32, _ld_of, _p, _plan_device,
+                        _same_device, get_transform)
 
 _DT = {torch.float32: K.KIN_F32, torch.float64: K.KIN_F64}
 _uid = itertools.count()
@@ -171,6 +171,82 @@ class CollisionPlan:
         K.check(K.lib().kin_coll_batch(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0), N, ptr(D), ldd,
                                        ptr(G), ldg, ptr(Mn), st))
         return D, G, Mn
+
+
+class CollisionIKPlan(Plan):
+    """kin_coll_ik_plan_create: the IK plan of `link` over `joints` with the checker's spheres staged on
+    the same chain -- both stages of inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
+    (src/inverse_kinematics.jl:1-21) for many targets per launch (``solve``).  It is also an ordinary IK
+    plan (``ik_dls``)."""
+
+    def __init__(self, sscc: SweptSphereCollisionChecker, link: Link, joints, dtype=torch.float32):
+        m = sscc.mech
+        m._sync_angles()
+        if dtype not in _DT:
+            raise TypeError("dtype must be torch.float32 or torch.float64")
+        self.m, self.dtype, self.sscc, self.link = m, dtype, sscc, link
+        self._q = _i32([j.id for j in joints])
+        self._o = _i32([link.id])
+        self._jl = link.id
+        self._j = self._q
+        self.zero_fill = True
+        self._s = _i32([l.id for l in sscc.sphere_links])
+        self._r = np.ascontiguousarray(np.asarray(sscc.sphere_radii, np.float64))
+        d = K.CollDesc(_DT[dtype], self._q.size, _p(self._q).value, self._s.size,
+                       _p(self._s).value if self._s.size else None, None, _p(self._r).value if self._s.size else None)
+        self._h = C.c_void_p()
+        K.check(K.lib().kin_coll_ik_plan_create(m._model, C.byref(d), link.id, C.byref(self._h)))
+        nq, rows, cols = C.c_int32(), C.c_int32(), C.c_int32()
+        K.check(K.lib().kin_plan_shape(self._h, C.byref(nq), C.byref(rows), C.byref(cols)))
+        self.n_qcols, self.jac_rows, self.jac_cols = nq.value, rows.value, cols.value
+        self.n_out = 1
+        self.n_sph = self._s.size
+        self.device_index = _current_device_index()
+
+    def specialize(self, kernels: int = 0) -> "CollisionIKPlan":
+        """kin_plan_specialize (default: both stages' kernels, KIN_SPEC_IK | KIN_SPEC_IK_COLL)."""
+        K.check(K.lib().kin_plan_specialize(self._h, int(kernels) or (K.KIN_SPEC_IK | K.KIN_SPEC_IK_COLL)))
+        return self
+
+    def ik_coll(self, sdf: UnionSDF, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
+                margin=0.02, band=0.0, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
+                max_step=0.5, with_rot=2, restarts=0, seed=0, index_base=0, stream=None):
+        """Stage 2 alone (kin_ik_coll_batch): from Q0 (or Q in place) -> (Q, iters [N], err [3, N]:
+        |dp|, |rot|, min sphere distance).  iters > max_iters: not converged."""
+        N = self._check_q(Q)
+        _plan_device(sdf, Q)
+        if Q0 is not None:
+            _same_device(Q0, Q, "Q0")
+            if Q0.shape != Q.shape or Q0.stride() != Q.stride() or Q0.dtype != Q.dtype:
+                raise ValueError("Q0 must have Q's shape, strides and dtype")
+        if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
+            raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
+        _same_device(targets, Q, "targets")
+        iters = torch.empty(N, dtype=torch.int32, device=Q.device)
+        err = torch.empty((3, N), dtype=self.dtype, device=Q.device)
+        prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
+                         int(restarts), int(seed), 0, int(index_base))
+        cp = K.IkCollParams(float(margin), float(band), float(weight), float(feas))
+        st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
+        K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                          (Q0 if Q0 is not None else Q).data_ptr(), Q.data_ptr(), Q.stride(0), N,
+                                          iters.data_ptr(), err.data_ptr(), N, st))
+        return Q, iters, err
+
+    def solve(self, sdf: UnionSDF, targets: torch.Tensor, Q0: torch.Tensor, use_bistage=True, margin=0.02,
+              with_rot=2, max_iters=64, restarts=3, seed=0, index_base=0, stream=None, **kw):
+        """Both stages on the device, no host round trip: stage 1 (use_bistage) = the collision-free
+        DLS (kin_ik_dls_batch_from, the seeds read from Q0), stage 2 = kin_ik_coll_batch from its
+        result (src/inverse_kinematics.jl:1-21).  -> (Q, iters, err [3, N]) of stage 2."""
+        Q = torch.empty_like(Q0)
+        ik_kw = {k: v for k, v in kw.items() if k in ("lam", "tol_pos", "tol_rot", "max_step")}
+        if use_bistage:
+            self.ik_dls(targets, Q, Q0=Q0, max_iters=max_iters, restarts=restarts, seed=seed, with_rot=with_rot,
+                        index_base=index_base, stream=stream, **ik_kw)
+            return self.ik_coll(sdf, targets, Q, margin=margin, with_rot=with_rot, max_iters=max_iters,
+                                restarts=restarts, seed=seed, index_base=index_base, stream=stream, **kw)
+        return self.ik_coll(sdf, targets, Q, Q0=Q0, margin=margin, with_rot=with_rot, max_iters=max_iters,
+                            restarts=restarts, seed=seed, index_base=index_base, stream=stream, **kw)
 
 
 def compute_coll_dists_(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, out_vals: np.ndarray):

@@ -716,29 +716,29 @@ def point_inverse_kinematics_nakamura(m: Mechanism, link: Link, joints, point_de
 
 
 def inverse_kinematics_(m: Mechanism, link: Link, joints, target_pose, sscc=None, sdf=None, use_bistage=True,
-                        ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2, max_step=0.5):
+                        ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2, max_step=0.5, solver="DLS"):
     """``inverse_kinematics!`` (src/inverse_kinematics.jl:1-30) -> (q, status); sets the mechanism's angles.
 
-    Without ``sscc`` / ``sdf`` (src/inverse_kinematics.jl:23-30): the DLS kernel, one iteration per
-    launch, stopped by the reference's ``ftol_abs`` rule (NLopt stops when one step changes the
-    objective by less than ftol): objective = |dp|^2 + |rot err|^2 (the DLS residual, an axis-angle
-    error where the reference uses rpy differences).  Status ``:FTOL_REACHED`` when that rule
+    Without ``sscc`` / ``sdf`` (src/inverse_kinematics.jl:23-30): the DLS kernel on the reference's
+    objective (f_objective: |[p* - p; rpy* - rpy]|^2, kin_ik_params.with_rot = 2), stopped by the
+    reference's ``ftol_abs`` rule (NLopt stops when one step changes the objective by less than
+    ftol): the k-th iterate is one launch of k steps from the starting angles (the solver's active
+    set lives inside the kernel), so the rule is checked after every step.  Status ``:FTOL_REACHED`` when that rule
     stopped it, ``:MAXEVAL_REACHED`` after ``max_iters`` steps.
 
     With ``sscc`` and ``sdf`` (src/inverse_kinematics.jl:1-21): the collision-aware form.  Stage 1
-    (``use_bistage``) is the collision-free solve above; stage 2 minimises the reference's objective
-    (sum of squared position + rpy differences, gradient -2 J_rpy^T diff) subject to the sphere
-    distances of ``IneqConst(sscc, joints, sdf, 1, 0.02)`` >= -1e-8 and the joint limits, with SLSQP
-    on the host (SciPy's; the reference uses NLopt's LD_SLSQP) and every evaluation on the GPU
-    (kin_pose_const_batch, kin_ineq_const_batch).  Status ``:FTOL_REACHED`` when SLSQP met its
-    ftol convergence test, else ``:MAXEVAL_REACHED`` / ``:FAILURE``.
+    (``use_bistage``) is the collision-free solve above; stage 2 solves the reference's objective
+    subject to the sphere distances of ``IneqConst(sscc, joints, sdf, 1, 0.02)`` and the joint limits:
+    by default on the GPU (``solver="DLS"``: the batched kin_ik_coll_batch kernel on a batch of one,
+    ``kinhip.CollisionIKPlan`` for many targets), or with SciPy's SLSQP on the host (``solver="SLSQP"``;
+    the reference uses NLopt's LD_SLSQP) over GPU evaluations.  See ``planning.collision_aware_ik``.
     """
     if (sscc is None) != (sdf is None):
         raise TypeError("inverse_kinematics_: pass both sscc and sdf (collision-aware form) or neither")
     if sscc is not None:
         from .planning import collision_aware_ik
         return collision_aware_ik(m, link, joints, target_pose, sscc, sdf, use_bistage=use_bistage, ftol=ftol,
-                                  with_rot=with_rot, max_iters=max_iters, lam=lam, max_step=max_step)
+                                  with_rot=with_rot, max_iters=max_iters, lam=lam, max_step=max_step, solver=solver)
     return _dls_ik_ftol(m, link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step)
 
 
@@ -748,20 +748,23 @@ def _dls_ik_ftol(m: Mechanism, link: Link, joints, target_pose, ftol, with_rot, 
     plan = _cached_plan(m, ("ik", link.id, tuple(j.id for j in joints)),
                         lambda: m.plan(joints, out_links=[link], jac_link=link, jac_joints=joints, with_rot=True,
                                        dtype=torch.float64), joints)
-    Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+    Q0 = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
     T = np.asarray(target_pose, np.float64)
     tgt = torch.tensor(T[:3, :4].T.reshape(12), device=dev).reshape(12, 1).contiguous()
-    kw = dict(lam=lam, tol_pos=0.0, tol_rot=0.0, max_step=max_step, with_rot=with_rot)
+    # the reference's objective (with_rot = 2: |[p* - p; rpy* - rpy]|^2, src/inverse_kinematics.jl:38-50)
+    kw = dict(lam=lam, tol_pos=0.0, tol_rot=0.0, max_step=max_step, with_rot=2 if with_rot else 0)
 
-    def objective(max_it):  # max_it = 0: evaluate only; 1: one DLS step, then evaluate
-        _, _, err = plan.ik_dls(tgt, Q, max_iters=max_it, **kw)
+    def state(k):  # the iterate after k DLS steps from Q0 (one launch; the active set lives in the kernel)
+        Q = torch.empty_like(Q0)
+        _, _, err = plan.ik_dls(tgt, Q, max_iters=k, Q0=Q0, **kw)
         e = err[:, 0].cpu().numpy()
-        return float(e[0] ** 2 + e[1] ** 2)
+        return Q, float(e[0] ** 2 + e[1] ** 2)
 
-    f = objective(0)
+    Q, f = state(0)
     status = ":MAXEVAL_REACHED"
-    for _ in range(int(max_iters)):
-        f_new = objective(1)
+    for k in range(1, int(max_iters) + 1):
+        Qn, f_new = state(k)
+        Q = Qn
         if abs(f - f_new) < ftol:
             status = ":FTOL_REACHED"
             break

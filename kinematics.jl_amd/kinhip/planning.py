@@ -279,24 +279,46 @@ def plan_trajectory(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF, q_
 
 def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: SweptSphereCollisionChecker,
                        sdf: UnionSDF, use_bistage=True, ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2,
-                       max_step=0.5, margin=0.02):
+                       max_step=0.5, margin=0.02, solver="DLS"):
     """``inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)`` (src/inverse_kinematics.jl:1-21);
-    see ``kinhip.inverse_kinematics_``.  -> (q, status); sets the mechanism's angles."""
-    from scipy.optimize import minimize
+    see ``kinhip.inverse_kinematics_``.  -> (q, status); sets the mechanism's angles.
+
+    ``solver="DLS"`` (default): stage 1 (use_bistage) is the collision-free solve with the reference's
+    ftol_abs rule (``_dls_ik_ftol``), stage 2 the batched collision-aware kernel
+    (``CollisionIKPlan.ik_coll``, kin_ik_coll_batch: the reference's rpy objective plus the
+    IneqConst(sscc, joints, sdf, 1, margin) sphere rows, 3 seeded restarts) on a batch of one, converged
+    to |dp|, |d rpy| < 1e-6 with every sphere at >= margin - 1e-6 (status ``:FTOL_REACHED``, else
+    ``:MAXEVAL_REACHED``).
+    ``solver="SLSQP"``: stage 2 by SciPy's SLSQP on the host (the reference uses NLopt's LD_SLSQP), one
+    GPU evaluation per iterate, ``ftol`` as the reference's ftol_abs."""
+    from .collision import CollisionIKPlan
     from .mechanism import _dls_ik_ftol
 
     if use_bistage:  # stage 1: the collision-free problem seeds stage 2 (src/inverse_kinematics.jl:8-13)
         _dls_ik_ftol(m, link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step)
     n_dof = len(joints) + (3 if m.with_base else 0)
     T = np.asarray(target_pose, np.float64).reshape(4, 4)
+    dev = _device()
+    tg = torch.tensor(np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]]), dtype=torch.float64,
+                      device=dev).reshape(12, 1)
+    if str(solver).upper() == "DLS":
+        plan = CollisionIKPlan(sscc, link, joints, dtype=torch.float64)
+        Q0 = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
+        Q = torch.empty_like(Q0)
+        Q, it, err = plan.ik_coll(sdf, tg.contiguous(), Q, Q0=Q0, margin=margin, with_rot=2 if with_rot else 0,
+                                  max_iters=max_iters, restarts=3, lam=lam, max_step=max_step, tol_pos=1e-6,
+                                  tol_rot=1e-6)
+        q = Q[:, 0].cpu().numpy()
+        m.set_joint_angles(joints, q)
+        return q, (":FTOL_REACHED" if int(it[0]) <= max_iters else ":MAXEVAL_REACHED")
+    if str(solver).upper() != "SLSQP":
+        raise ValueError(f"unknown solver {solver!r} (DLS or SLSQP)")
+    from scipy.optimize import minimize
     # objective: PoseConstraint's residual [p - p*; rpy - rpy*] and its rpy Jacobian on the GPU
     pc = PoseConstraint(1, n_dof, link, T, with_rot, m, joints, dtype=torch.float64)
     # src/inverse_kinematics.jl:16 (a checker without spheres has no constraints: the reference's own
     # PR2 test builds one, test/test_inverse_kinematics.jl:63, with an un-iterated generator)
     G = IneqConst(sscc, joints, sdf, 1, margin, dtype=torch.float64) if sscc.sphere_links else None
-    dev = _device()
-    tg = torch.tensor(np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]]), dtype=torch.float64,
-                      device=dev).reshape(12, 1)
     rel = np.array([m.is_relevant(j, link) for j in joints] + [True] * (n_dof - len(joints)))
 
     def pose_eval(x):
@@ -325,13 +347,9 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
     lo = [j.lower_limit for j in joints] + [-np.inf] * (n_dof - len(joints))
     hi = [j.upper_limit for j in joints] + [np.inf] * (n_dof - len(joints))
     x0 = np.clip(m.get_joint_angles(joints), lo, hi)
-    # SciPy's SLSQP stops on |f - f_prev| < ftol once feasible.  Stage 2 starts at the stage-1 optimum
-    # (f ~ 0, infeasible) and met that test with the pose still ~sqrt(ftol) off (1e-3 at ftol 1e-5:
-    # tools/cik_probe.py); NLopt reaches its ftol_abs stop after the quadratic tail.  Stage 2 therefore
-    # runs at ftol^2, i.e. the same ftol on the residual norm instead of its square.
     cons = [{"type": "ineq", "fun": lambda x: go(x)[0], "jac": lambda x: go(x)[1]}] if G is not None else []
     res = minimize(lambda x: fo(x)[0], x0, jac=lambda x: fo(x)[1], method="SLSQP", bounds=list(zip(lo, hi)),
-                   constraints=cons, options={"ftol": ftol * ftol, "maxiter": max_iters})
+                   constraints=cons, options={"ftol": ftol, "maxiter": max_iters})  # ftol_abs, as the reference
     q = np.asarray(res.x, np.float64)
     m.set_joint_angles(joints, q)
     status = ":FTOL_REACHED" if res.success else (":MAXEVAL_REACHED" if res.status == 9 else ":FAILURE")

@@ -866,3 +866,171 @@ void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, con
         or_mech_destroy(m);
     }
 }
+
+/* ---- build-defined collision-aware IK (kin_ik_coll_batch), restated for parity ----
+ * Stage 2 of inverse_kinematics!(m, link, joints, target, sscc, sdf) (src/inverse_kinematics.jl:1-21)
+ * as the GPU kernel does it (kinhip_ikc_dev.h): per iteration the pose residual e (with_rot as in
+ * or_ik_dls_batch) and, for every sphere with d_k < margin + band, the IneqConst row a_k = grad sdf^T J_k
+ * (analytic gradient of the argmin box); one damped Gauss-Newton step on the normal equations
+ *   (J^T J + w^2 sum a_k^T a_k + lambda^2 I) dq = J^T e + w^2 sum a_k^T (margin + band - d_k)
+ * over the joints (+ base), joints held out while on a limit and pushed outward (by the last step, or by
+ * the right-hand side while held), |dq|_inf <= max_step, clamp; converged when |dp| < tol_pos,
+ * |rot| < tol_rot and every d_k >= margin - feas. */
+static void box_gradient_analytic(const or_union_sdf* s, int32_t k, const double* p, double g[3]) {
+    const double* T = s->inv_pose + 16 * k;
+    double l[3], q[3], gl[3];
+    for (int i = 0; i < 3; ++i) {
+        l[i] = T[12 + i] + (T[i] * p[0] + T[4 + i] * p[1] + T[8 + i] * p[2]);
+        q[i] = fabs(l[i]) - 0.5 * s->width[3 * k + i];
+    }
+    double mx = q[0] > q[1] ? q[0] : q[1];
+    mx = q[2] > mx ? q[2] : mx;
+    if (mx > 0) {
+        double o[3], nn = 0;
+        for (int i = 0; i < 3; ++i) { o[i] = q[i] > 0 ? q[i] : 0.0; nn += o[i] * o[i]; }
+        nn = sqrt(nn);
+        for (int i = 0; i < 3; ++i) gl[i] = (l[i] < 0 ? -o[i] : o[i]) / nn;
+    } else {
+        int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
+        for (int i = 0; i < 3; ++i) gl[i] = i == im ? (l[i] < 0 ? -1.0 : 1.0) : 0.0;
+    }
+    for (int j = 0; j < 3; ++j) g[j] = T[4 * j] * gl[0] + T[4 * j + 1] * gl[1] + T[4 * j + 2] * gl[2];
+}
+
+void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, double* q, int64_t ldq, int32_t n_q,
+                      const int32_t* qids, int32_t link_id, const double* target, int64_t ldt, const or_ik_params* prm,
+                      const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii, int32_t* iters_out,
+                      double* err_out, int32_t n_threads) {
+    int nt = nthreads_of(n_threads);
+    const int32_t nd = n_q + (proto->with_base ? 3 : 0);
+    const int rows = prm->with_rot ? 6 : 3;
+    const double margin = cprm[0], band = cprm[1], w2 = cprm[2] * cprm[2], feas = cprm[3];
+#pragma omp parallel num_threads(nt)
+    {
+        or_mech* m = or_mech_clone(proto);
+        double* a = (double*)malloc(sizeof(double) * (nd + 1));
+        double* J = (double*)malloc(sizeof(double) * 6 * (nd + 1));
+        double* J3 = (double*)malloc(sizeof(double) * 3 * (nd + 1));
+        double* A = (double*)malloc(sizeof(double) * (nd + 1) * (nd + 1));
+        double* bv = (double*)malloc(sizeof(double) * (nd + 1));
+        double* y = (double*)malloc(sizeof(double) * (nd + 1));
+        double* av = (double*)malloc(sizeof(double) * (nd + 1));
+        double* lo = (double*)malloc(sizeof(double) * (nd + 1));
+        double* hi = (double*)malloc(sizeof(double) * (nd + 1));
+        int* rel = (int*)malloc(sizeof(int) * (nd + 1));
+        for (int32_t c = 0; c < nd; ++c) {
+            rel[c] = c >= n_q || or_is_relevant(m, qids[c], link_id);
+            lo[c] = c < n_q && rel[c] ? m->jlower[qids[c] - 1] : -INFINITY;
+            hi[c] = c < n_q && rel[c] ? m->jupper[qids[c] - 1] : INFINITY;
+        }
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < n; ++i) {
+            tf_t tgt = tf_identity();
+            for (int k = 0; k < 12; ++k) tgt.m[(k / 3) * 4 + (k % 3)] = target[(size_t)k * ldt + i];
+            double trpy[3];
+            rpy_of(&tgt, trpy);
+            for (int32_t c = 0; c < nd; ++c) a[c] = q[c * ldq + i];
+            double a0[64];
+            int held[64];
+            for (int32_t c = 0; c < nd; ++c) { a0[c] = a[c]; held[c] = 0; }
+            const int32_t attempt_len = prm->restarts > 0 ? prm->max_iters / (prm->restarts + 1) : 0;
+            int32_t it = 0;
+            int conv = 0;
+            double ep = 0, er = 0, dmin = INFINITY;
+            for (;; ++it) {
+                or_set_joint_angles(m, n_q, qids, a);
+                memset(A, 0, sizeof(double) * nd * nd);
+                memset(bv, 0, sizeof(double) * nd);
+                dmin = INFINITY;
+                for (int32_t k = 0; k < n_sph; ++k) {
+                    tf_t t = get_transform(m, sph[k]);
+                    double p[3] = {M(t, 0, 3), M(t, 1, 3), M(t, 2, 3)};
+                    int32_t kb = 0;
+                    const double d = or_union_sdf_value(sdf, p, &kb) - radii[k];
+                    if (d < dmin) dmin = d;
+                    const double viol = margin + band - d;
+                    if (viol > 0) {
+                        double g[3];
+                        box_gradient_analytic(sdf, kb, p, g);
+                        memset(J3, 0, sizeof(double) * 3 * nd);
+                        or_get_jacobian(m, sph[k], n_q, qids, 0, 0, J3);
+                        for (int32_t c = 0; c < nd; ++c) av[c] = g[0] * J3[3 * c] + g[1] * J3[3 * c + 1] + g[2] * J3[3 * c + 2];
+                        for (int32_t r = 0; r < nd; ++r) {
+                            bv[r] += w2 * av[r] * viol;
+                            for (int32_t c = 0; c < nd; ++c) A[r + nd * c] += w2 * av[r] * av[c];
+                        }
+                    }
+                }
+                tf_t now = get_transform(m, link_id);
+                double e[6];
+                for (int k = 0; k < 3; ++k) e[k] = M(tgt, k, 3) - M(now, k, 3);
+                if (prm->with_rot == 2) {
+                    double rn[3];
+                    rpy_of(&now, rn);
+                    for (int k = 0; k < 3; ++k) {
+                        const double dd = trpy[k] - rn[k];
+                        e[3 + k] = dd - 6.283185307179586476925286766559 * rint(dd * 0.15915494309189533576888376337251);
+                    }
+                } else if (prm->with_rot) {
+                    rot_error(&tgt, &now, e + 3);
+                }
+                ep = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+                er = prm->with_rot ? sqrt(e[3] * e[3] + e[4] * e[4] + e[5] * e[5]) : 0.0;
+                if (ep < prm->tol_pos && er < prm->tol_rot && dmin >= margin - feas) { conv = 1; break; }
+                if (it >= prm->max_iters) break;
+                if (attempt_len > 0 && it > 0 && it % attempt_len == 0) {
+                    const int32_t att = it / attempt_len;
+                    for (int32_t c = 0; c < nd; ++c) {
+                        if (c < n_q && rel[c]) {
+                            double l = lo[c], h = hi[c];
+                            if (!isfinite(l) || !isfinite(h)) { l = -3.14159265358979323846; h = 3.14159265358979323846; }
+                            a[c] = l + (h - l) * or_ik_seed_u01(prm->seed, i, att, c);
+                        } else {
+                            a[c] = a0[c];
+                        }
+                        held[c] = 0;
+                    }
+                    continue;
+                }
+                memset(J, 0, sizeof(double) * 6 * nd);
+                or_get_jacobian(m, link_id, n_q, qids, prm->with_rot != 0, prm->with_rot == 2, J);
+                for (int32_t r = 0; r < nd; ++r) {
+                    for (int k = 0; k < rows; ++k) bv[r] += J[k + rows * r] * e[k];
+                    for (int32_t c = 0; c < nd; ++c) {
+                        double s2 = 0;
+                        for (int k = 0; k < rows; ++k) s2 += J[k + rows * r] * J[k + rows * c];
+                        A[r + nd * c] += s2;
+                    }
+                }
+                for (int32_t r = 0; r < nd; ++r) {
+                    const int fr = rel[r] && !held[r];
+                    for (int32_t c = 0; c < nd; ++c)
+                        if (c != r && (!fr || !(rel[c] && !held[c]))) A[r + nd * c] = 0.0;
+                    A[r + nd * r] = fr ? A[r + nd * r] + prm->lambda * prm->lambda : 1.0;
+                    y[r] = fr ? bv[r] : 0.0;
+                }
+                chol_solve(A, nd, y);
+                double mx = 0;
+                for (int32_t c = 0; c < nd; ++c) {
+                    if (c < n_q && rel[c]) {
+                        const double dir = held[c] ? bv[c] : y[c];
+                        const int nh = (a[c] <= lo[c] && dir < 0) || (a[c] >= hi[c] && dir > 0);
+                        if (held[c]) y[c] = 0.0;
+                        held[c] = nh;
+                    }
+                    if (fabs(y[c]) > mx) mx = fabs(y[c]);
+                }
+                const double sc = mx > prm->max_step ? prm->max_step / mx : 1.0;
+                for (int32_t c = 0; c < nd; ++c) {
+                    const double v = a[c] + sc * y[c];
+                    a[c] = v < lo[c] ? lo[c] : (v > hi[c] ? hi[c] : v);
+                }
+            }
+            for (int32_t c = 0; c < nd; ++c) q[c * ldq + i] = a[c];
+            if (iters_out) iters_out[i] = conv ? it : prm->max_iters + 1;
+            if (err_out) { err_out[i] = ep; err_out[n + i] = er; err_out[2 * n + i] = dmin; }
+        }
+        free(a); free(J); free(J3); free(A); free(bv); free(y); free(av); free(lo); free(hi); free(rel);
+        or_mech_destroy(m);
+    }
+}

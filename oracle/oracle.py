@@ -197,6 +197,7 @@ def lib():
         L.or_union_sdf_value.argtypes = [P, P, P]
         L.or_union_sdf_gradient.argtypes = [P, P, P]
         L.or_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, P, D, P, I64, P, I64, I32]
+        L.or_ik_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, I64, P, P, I32, P, P, P, P, I32]
         _lib = L
     return _lib
 
@@ -339,6 +340,26 @@ class OracleMech:
         lib().or_ik_dls_batch(self._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt), tgt.shape[1],
                               C.byref(prm), _p(it), _p(err), n_threads)
         return q, it, err
+
+
+def ik_coll_batch(mech: "OracleMech", sdf: "OracleUnionSDF", q0, q_joint_ids, link_id, target, sphere_links, radii,
+                  margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
+                  max_step=0.5, with_rot=2, restarts=0, seed=0, n_threads=0):
+    """Restatement of kin_ik_coll_batch (stage 2 of the bistage collision-aware IK) -> (q, iters, err [3, N])."""
+    q = _f64(q0).copy()
+    ids = _i32(q_joint_ids)
+    tgt = _f64(target)
+    sph = _i32(sphere_links)
+    r = _f64(radii)
+    N = q.shape[1]
+    it = np.zeros(N, np.int32)
+    err = np.zeros((3, N))
+    prm = _IkParams(max_iters, lam, tol_pos, tol_rot, max_step, int(with_rot), int(restarts), int(seed))
+    cp = _f64([margin, band, weight, feas])
+    lib().or_ik_coll_batch(mech._h, sdf._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt), tgt.shape[1],
+                           C.byref(prm), _p(cp), sph.size, _p(sph) if sph.size else None, _p(r) if sph.size else None,
+                           _p(it), _p(err), n_threads)
+    return q, it, err
 
 
 def rot_error(T_target, T_now):

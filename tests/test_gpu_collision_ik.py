@@ -110,3 +110,146 @@ def test_collision_ik_argument_errors():
     m, arm, sscc, sdf = _scene()
     with pytest.raises(TypeError):
         kinhip.inverse_kinematics_(m, m.find_link("gripper_link"), arm, np.eye(4), sscc, None)
+
+
+def _oracle_scene(sdf):
+    import oracle as O
+    tree = O.parse_urdf_tree(golden("fetch.urdf"))
+    om = O.OracleMech(tree)
+    sph, rad = [], []
+    for name, c, r in kinhip.FETCH_ARM_SPHERES:
+        T = np.eye(4)
+        T[:3, 3] = c
+        sph.append(om.add_new_link(tree.link_id(name), T))
+        rad.append(r)
+    box = O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+    return O, tree, om, sph, rad, box
+
+
+def _check_batch(sdf, tg, Q, it, err, max_iters, dtype, min_conv):
+    """Converged targets (iters <= max_iters) meet the reference's acceptance, recomputed by the oracle
+    at the returned angles: |dp| < 1e-3, |d rpy| < 1e-3, every sphere >= margin - 1e-6 (fp32: 1e-5), within
+    the joint limits."""
+    O, tree, om, sph, rad, box = _oracle_scene(sdf)
+    ids = [tree.joint_id(n) for n in ARM]
+    gl = tree.link_id("gripper_link")
+    conv = it.cpu().numpy() <= max_iters
+    assert conv.mean() >= min_conv, conv.mean()
+    q = Q.double().cpu().numpy()
+    got = om.fk_batch(q, ids, [gl])[0]
+    T = tg.double().cpu().numpy()
+    dp = np.linalg.norm(got[9:] - T[9:], axis=0)
+    assert np.all(dp[conv] < 1e-3), dp[conv].max()
+    for k in np.nonzero(conv)[0][:: max(1, conv.sum() // 512)]:  # rpy on a sample (host loop)
+        Ta, Tt = np.eye(4), np.eye(4)
+        Ta[:3, :4] = got[:, k].reshape(4, 3).T
+        Tt[:3, :4] = T[:, k].reshape(4, 3).T
+        d = O.rpy(Ta) - O.rpy(Tt)
+        assert np.all(np.abs((d + np.pi) % (2 * np.pi) - np.pi) < 1e-3), (k, d)
+    dist, _ = O.coll_batch(om, box, q, ids, sph, rad, with_grad=False)
+    ftol = 1e-6 if dtype == torch.float64 else 1e-5
+    assert np.all(dist[:, conv] >= 0.02 - ftol), dist[:, conv].min()
+    np.testing.assert_allclose(err[2].double().cpu().numpy()[conv], dist.min(0)[conv], atol=1e-5)
+    lo = np.nan_to_num(np.array([kinhip.parse_urdf(golden("fetch.urdf")).find_joint(n).lower_limit for n in ARM]),
+                       neginf=-1e9)
+    hi = np.nan_to_num(np.array([kinhip.parse_urdf(golden("fetch.urdf")).find_joint(n).upper_limit for n in ARM]),
+                       posinf=1e9)
+    tol = 1e-6 if dtype == torch.float32 else 0
+    assert np.all(q >= lo[:, None] - tol) and np.all(q <= hi[:, None] + tol)
+    return conv
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_batched_collision_ik_in_fridge(dtype):
+    """the bistage solve of test_bistage_ik_in_fridge for 4,096 targets in one launch per
+    stage (CollisionIKPlan.solve: kin_ik_dls_batch_from, then kin_ik_coll_batch), targets spread over
+    the fridge's open upper compartment (x 0.9..1.05, y +-0.12, z 1.15..1.32, yaw +-0.3)."""
+    m, arm, sscc, sdf = _scene()
+    gl = m.find_link("gripper_link")
+    dev = torch.device("cuda", 0)
+    N = 4096
+    rng = np.random.default_rng(17)
+    tg = np.zeros((12, N))
+    for k in range(N):
+        T = _pose((rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32)), rng.uniform(-0.3, 0.3))
+        tg[:, k] = np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+    tg = torch.tensor(tg, dtype=dtype, device=dev).contiguous()
+    plan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dtype).specialize()
+    Q0 = torch.zeros((8, N), dtype=dtype, device=dev)
+    Q, it, err = plan.solve(sdf, tg, Q0, max_iters=128, restarts=3, seed=1)
+    conv = _check_batch(sdf, tg, Q, it, err, 128, dtype, 0.9)
+    # stage 1 alone would collide for some of them: the constraint did work
+    print(f"batched bistage in the fridge {dtype}: converged {conv.mean():.4f}")
+
+
+@pytest.mark.parametrize("target,link,size", [((0.75, 0.15, 1.0), "elbow_flex_link", 0.08),
+                                              ((0.7, -0.2, 1.1), "elbow_flex_link", 0.08),
+                                              ((0.8, 0.0, 1.2), "upperarm_roll_link", 0.08),
+                                              ((0.6, 0.3, 0.9), "forearm_roll_link", 0.06)])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_batched_collision_ik_pillar(target, link, size, dtype):
+    """test_bistage_ik_moves_the_arm_off_an_obstacle as a batch: 4,096 targets jittered by +-5 mm around
+    the case's target, the pillar on the stage-1 solution's link (so stage 1 collides for most of them);
+    both stages for all of them in one launch each, and every converged solution is off the pillar
+    at the pose."""
+    m, arm, sscc, sdf0 = _scene()
+    gl = m.find_link("gripper_link")
+    T0 = _pose(target)
+    m.set_joint_angles(arm, np.zeros(8))
+    kinhip.inverse_kinematics_(m, gl, arm, T0)
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(_pose(kinhip.get_transform(m, m.find_link(link))[:3, 3]),
+                                                     (size, size, size))])
+    dev = torch.device("cuda", 0)
+    N = 4096
+    rng = np.random.default_rng(5)
+    tg = np.zeros((12, N))
+    for k in range(N):
+        T = _pose(np.asarray(target) + rng.uniform(-0.005, 0.005, 3))
+        tg[:, k] = np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+    tg = torch.tensor(tg, dtype=dtype, device=dev).contiguous()
+    plan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dtype).specialize()
+    Q0 = torch.zeros((8, N), dtype=dtype, device=dev)
+    Q1 = torch.empty_like(Q0)
+    plan.ik_dls(tg, Q1, Q0=Q0, max_iters=64, restarts=3, seed=1, with_rot=2)
+    _, _, D1 = sscc.plan(arm, dtype=dtype).run(sdf, Q1, dists=False, min_dist=True)
+    Q, it, err = plan.solve(sdf, tg, Q0, max_iters=128, restarts=3, seed=1)
+    conv = _check_batch(sdf, tg, Q, it, err, 128, dtype, 0.99)
+    print(f"pillar {target} {dtype}: stage-1 solutions under the margin {float((D1 < 0.02).float().mean()):.3f}, "
+          f"bistage converged {conv.mean():.4f}")
+    assert float((D1 < 0.02).float().mean()) > 0.4
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_collision_ik_iterates_vs_oracle(spec):
+    """kin_ik_coll_batch (fp64) vs its CPU restatement (oracle or_ik_coll_batch): from the same seeds
+    (the GPU's stage-1 solutions of 512 fridge targets) the same iteration counts, angles within 1e-7,
+    errors and minimum sphere distances within 1e-9 -- generic and plan-specialised kernels, the
+    reference's rpy objective with restarts."""
+    import oracle as O
+    m, arm, sscc, sdf = _scene()
+    gl = m.find_link("gripper_link")
+    dev = torch.device("cuda", 0)
+    N = 512
+    rng = np.random.default_rng(23)
+    tg = np.zeros((12, N))
+    for k in range(N):
+        T = _pose((rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32)), rng.uniform(-0.3, 0.3))
+        tg[:, k] = np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    plan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=torch.float64)
+    if spec:
+        plan.specialize()
+    Q0 = torch.zeros((8, N), dtype=torch.float64, device=dev)
+    Q1 = torch.empty_like(Q0)
+    plan.ik_dls(tgt, Q1, Q0=Q0, max_iters=64, restarts=3, seed=2, with_rot=2)  # stage 1 (seeds for both)
+    kw = dict(margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=96, lam=1e-2, tol_pos=1e-4, tol_rot=1e-4,
+              max_step=0.5, with_rot=2, restarts=2, seed=7)
+    Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, **kw)
+    O_, tree, om, sph, rad, box = _oracle_scene(sdf)
+    ids = [tree.joint_id(n) for n in ARM]
+    rq, rit, rerr = O.ik_coll_batch(om, box, Q1.cpu().numpy(), ids, tree.link_id("gripper_link"), tg, sph, rad, **kw)
+    it = it.cpu().numpy()
+    assert (it <= 96).mean() > 0.8
+    np.testing.assert_array_equal(it, rit)
+    np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+    np.testing.assert_allclose(err.cpu().numpy(), rerr, atol=1e-9)
