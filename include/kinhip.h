@@ -301,6 +301,17 @@ typedef struct kin_sdf kin_sdf;
 KINHIP_API int kin_sdf_create_boxes(int32_t n_boxes, const double* poses16, const double* widths3, kin_sdf** out);
 KINHIP_API int kin_sdf_destroy(kin_sdf* s);
 
+/* UnionSDF(mech) of a scene mechanism (src/sdf.jl:76-97): box k = BoxSDF(origin, width) attached to link
+ * link_ids[k] of `scene` (attach_to_link, :43-46), its world pose get_transform(scene, link) * origin
+ * (:14-32) -- e.g. the fridge's door box follows door_joint.  The scene joints q_joint_ids (+ the scene's
+ * planar base when the scene model has with_base) are inputs of every kin_coll_batch_scene call; other
+ * scene joints are held at the scene model's angles (kin_model_set_angles) as of this call.  Boxes ride
+ * on at most 4 moving frames (the root / base and the child frames of batch joints).  Uploaded to the
+ * current device in both precisions. */
+KINHIP_API int kin_sdf_create_attached(const kin_model* scene, int32_t n_q, const int32_t* q_joint_ids,
+                                       int32_t n_boxes, const int32_t* link_ids, const double* origins16,
+                                       const double* widths3, kin_sdf** out);
+
 typedef struct kin_coll_desc {
     int32_t dtype;
     int32_t n_q;                     /* batch columns (+3 base) and gradient columns */
@@ -332,6 +343,14 @@ KINHIP_API int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* des
 KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq,
                               int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
                               void* stream);
+
+/* kin_coll_batch against boxes attached to a scene (kin_sdf_create_attached): scene_q [n_scene_cols][lds]
+ * holds the scene joint values (+ base x, y, theta) of every sample -- one launch sweeps e.g. many door
+ * angles -- or, with lds = 0, one set of values for the whole launch.  Plain SoA only; the generic
+ * kernel runs (no plan specialisation for attached boxes). */
+KINHIP_API int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q,
+                                    int64_t ldq, const void* scene_q, int64_t lds, int64_t n, void* dists,
+                                    int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream);
 
 /* kin_coll_batch on the tiled layout (see kin_plan_run_tiled): element (config i,
  * row r) of q / dists / grads / min_dist at X[(i / tile) * ts + r * ld + i % tile]

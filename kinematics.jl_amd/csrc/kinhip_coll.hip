@@ -18,7 +18,57 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
     coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem);
 }
 
+// the same with the union's boxes attached to a scene mechanism (kin_coll_batch_scene; generic only)
+template <typename T, int MAXA, bool GRAD>
+__global__ __launch_bounds__(256) void k_coll_scene(const KProg<T> P, const KStep<T>* __restrict__ S,
+                                                    const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
+                                                    const CollArgs a, const T* __restrict__ q, int64_t ldq, int64_t n,
+                                                    T* __restrict__ dists, int64_t ldd, T* __restrict__ grads,
+                                                    int64_t ldg, T* __restrict__ min_dist, const Tiling tl,
+                                                    const SceneArgs<T> sa) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    coll_body<T, MAXA, GRAD, true>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem, sa);
+}
+
 }  // namespace
+
+template <typename T>
+hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                             const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
+                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st) {
+    const Tiling tl{0xffffffffu, 0, 0, 0, 0};
+    const size_t lds = grads && a.n_boxes <= kCollLdsBoxes ? (size_t)a.n_boxes * sizeof(KBox<T>) : 0;
+    for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
+        const int64_t c = std::min(kChunk, n - s0);
+        const dim3 grid(grid_of(c, 256)), block(256);
+        SceneArgs<T> sa;
+        sa.groups = (const KSceneGroup*)sl.groups;
+        sa.steps = (const KSceneStep<T>*)sl.steps;
+        sa.q = (const T*)sl.q + (sl.uniform ? 0 : s0);
+        sa.ld = sl.ld;
+        sa.ng = sl.ng;
+        sa.base_col = sl.base_col;
+        sa.uniform = sl.uniform;
+        const T* qc = q + s0;
+        T* dc = dists ? dists + s0 : dists;
+        T* gc = grads ? grads + s0 : grads;
+        T* mc = min_dist ? min_dist + s0 : min_dist;
+#define KIN_COS_LAUNCH(MA) \
+        hipLaunchKernelGGL((k_coll_scene<T, MA, false>), grid, block, lds, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl, sa)
+#define KIN_COSG_LAUNCH(MA) \
+        hipLaunchKernelGGL((k_coll_scene<T, MA, true>), grid, block, lds, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl, sa)
+        if (grads) {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_COSG_LAUNCH)
+        } else {
+            KIN_MAXA_DISPATCH(g.maxA, KIN_COS_LAUNCH)
+        }
+#undef KIN_COS_LAUNCH
+#undef KIN_COSG_LAUNCH
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 template <typename T>
 hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
@@ -69,7 +119,10 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
 #define KIN_INSTANTIATE(T)                                                                                    \
     template hipError_t launch_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,   \
                                        const LaunchGeom&, const CollArgs&, const T*, int64_t, int64_t, T*,    \
-                                       int64_t, T*, int64_t, T*, const TileArgs&, const JitFns*, hipStream_t);
+                                       int64_t, T*, int64_t, T*, const TileArgs&, const JitFns*, hipStream_t); \
+    template hipError_t launch_coll_scene<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, \
+                                             const LaunchGeom&, const CollArgs&, const SceneLaunch&, const T*,        \
+                                             int64_t, int64_t, T*, int64_t, T*, int64_t, T*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

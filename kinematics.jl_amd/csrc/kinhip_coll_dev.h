@@ -136,6 +136,121 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
     }
 }
 
+// ---- boxes attached to a scene mechanism (kin_sdf_create_attached, kinhip_prog.h KSceneStep) ----
+template <typename T>
+struct SceneArgs {
+    const KSceneGroup* groups = nullptr;
+    const KSceneStep<T>* steps = nullptr;
+    const T* q = nullptr;    // scene columns [cols][ld] (per sample), or one sample for the whole launch
+    int64_t ld = 0;
+    int32_t ng = 0;
+    int32_t base_col = -1;   // scene planar base (x, y, theta) columns, -1: none
+    int32_t uniform = 0;     // 1: every sample uses the scene column values of sample 0
+};
+template <typename T>
+struct SceneCtx {
+    const KSceneGroup* groups;
+    int ng;
+    T inv[kMaxSceneGroups][12];  // per lane: world -> group frame (row-major 3x4)
+};
+
+// rotation by th about the unit axis u (Rodrigues; the reference's UnitQuaternion(cos th/2, u sin th/2))
+template <typename T>
+__device__ __forceinline__ void axis_rotation(const T* __restrict__ u, T th, T (&R)[9]) {
+    T s, c;
+    sincos_t(th, &s, &c);
+    const T v = T(1) - c, x = u[0], y = u[1], z = u[2];
+    R[0] = fma(x * x, v, c);     R[1] = fma(x * y, v, -z * s); R[2] = fma(x * z, v, y * s);
+    R[3] = fma(y * x, v, z * s); R[4] = fma(y * y, v, c);      R[5] = fma(y * z, v, -x * s);
+    R[6] = fma(z * x, v, -y * s); R[7] = fma(z * y, v, x * s); R[8] = fma(z * z, v, c);
+}
+
+// the group frames of this sample (get_transform(scene, link) up to the group's moving frame), inverted
+template <typename T>
+__device__ __forceinline__ void scene_frames(SceneCtx<T>& sc, const SceneArgs<T>& sa, uint32_t off) {
+    sc.groups = sa.groups;
+    sc.ng = sa.ng;
+    const uint32_t so = sa.uniform ? 0u : off;
+#pragma unroll
+    for (int g = 0; g < kMaxSceneGroups; ++g) {
+        if (g >= sa.ng) break;  // uniform
+        const KSceneGroup& G = sa.groups[g];
+        Fr<T> f;
+        if (sa.base_col >= 0)
+            base_frame(f, ld_soa(sa.q, sa.base_col, sa.ld, so), ld_soa(sa.q, sa.base_col + 1, sa.ld, so),
+                       ld_soa(sa.q, sa.base_col + 2, sa.ld, so));
+        else
+            set_identity(f);
+        for (int k = G.step0; k < G.step1; ++k) {
+            const KSceneStep<T>& st = sa.steps[k];
+            mul_rigid(f, st.F);
+            if (st.kind == MOT_REV) {
+                T R[9];
+                axis_rotation(st.axis, ld_soa(sa.q, st.qcol, sa.ld, so), R);
+                Fr<T> h;
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j)
+                        h.r[3 * i + j] = fma(f.r[3 * i], R[j], fma(f.r[3 * i + 1], R[3 + j], f.r[3 * i + 2] * R[6 + j]));
+#pragma unroll
+                for (int k2 = 0; k2 < 9; ++k2) f.r[k2] = h.r[k2];
+            } else if (st.kind == MOT_PRISM) {
+                const T d = ld_soa(sa.q, st.qcol, sa.ld, so);
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    f.t[i] = fma(fma(f.r[3 * i], st.axis[0], fma(f.r[3 * i + 1], st.axis[1], f.r[3 * i + 2] * st.axis[2])), d,
+                                 f.t[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) sc.inv[g][4 * i + j] = f.r[3 * j + i];
+            sc.inv[g][4 * i + 3] = -fma(f.r[i], f.t[0], fma(f.r[3 + i], f.t[1], f.r[6 + i] * f.t[2]));
+        }
+    }
+}
+
+// UnionSDF over the scene's groups: each group's boxes in its own frame (union_sdf), the first minimum
+// over groups; the gradient rotated back to the world
+template <typename T, bool GRAD, int NS>
+__device__ __forceinline__ void scene_union(const SceneCtx<T>& sc, const KBox<T>* __restrict__ boxes,
+                                            const KAabb<T>* __restrict__ aabb, const T (&px)[NS], const T (&py)[NS],
+                                            const T (&pz)[NS], T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem,
+                                            bool use_lds) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        d[i] = T(INFINITY);
+        gw[i][0] = gw[i][1] = gw[i][2] = T(0);
+    }
+#pragma unroll
+    for (int g = 0; g < kMaxSceneGroups; ++g) {
+        if (g >= sc.ng) break;  // uniform
+        const KSceneGroup& G = sc.groups[g];
+        const T* I = sc.inv[g];
+        T lx[NS], ly[NS], lz[NS], dg[NS], gg[NS][3];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            lx[i] = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
+            ly[i] = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
+            lz[i] = fma(I[8], px[i], fma(I[9], py[i], fma(I[10], pz[i], I[11])));
+        }
+        union_sdf<T, GRAD, NS>(boxes + G.box0, aabb + G.aabb0, G.na, G.nb, lx, ly, lz, dg, gg,
+                               smem + (size_t)G.box0 * sizeof(KBox<T>), use_lds);
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (dg[i] < d[i]) {
+                d[i] = dg[i];
+                if (GRAD) {  // world gradient = R_g g_local, R_g = (inverse rotation)^T
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) gw[i][j] = fma(I[j], gg[i][0], fma(I[4 + j], gg[i][1], I[8 + j] * gg[i][2]));
+                }
+            }
+        }
+    }
+}
+
 // Two spheres of a link per pass over the boxes (coll_spheres): 1 = in the min-distance kernel only
 // (default), 2 = in both kernels, 0 = never.  The pair costs ~15 VGPRs: the min-distance kernel keeps
 // 8 waves per SIMD and gains ~2% (fewer scalar box loads and waits); the gradient kernel would drop
@@ -154,7 +269,7 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
 #define KINHIP_JIT 0
 #endif
 
-template <typename T, int MAXA, bool GRAD>
+template <typename T, int MAXA, bool GRAD, bool SCENE = false>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
                                              const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
                                              const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb,
@@ -162,7 +277,8 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              const T (&rm)[MAXA][3], const T (&rz)[MAXA][3], T bx, T by,
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
                                              T* __restrict__ grads, int64_t ldg, T& dmin,
-                                             const unsigned char* smem, bool use_lds) {
+                                             const unsigned char* smem, bool use_lds,
+                                             const SceneCtx<T>* sc = nullptr) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
     // paired stores (KINHIP_COLL_STPAIR): every lane of the wave active, rows 8-byte aligned
     const bool pair_ok = GRAD && KINHIP_COLL_STPAIR && grads && (ldg & 1) == 0 &&
@@ -297,7 +413,8 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         // skip only when both spheres are beyond the truncation wave-wide (the exact path gives the
         // same results for one that is)
         const bool far = all_far(sph[k], px[0], py[0], pz[0]) && all_far(sph[k + 1], px[1], py[1], pz[1]);
-        if (!far) union_sdf<T, GRAD, 2>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
+        if constexpr (SCENE) scene_union<T, GRAD, 2>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
+        else if (!far) union_sdf<T, GRAD, 2>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
         finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
         finish(sph[k + 1], px[1], py[1], pz[1], far, ds[1], g[1]);
     }
@@ -305,17 +422,19 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         T px[1], py[1], pz[1], ds[1] = {T(0)}, g[1][3] = {{T(0), T(0), T(0)}};
         centre(sph[k], px[0], py[0], pz[0]);
         const bool far = all_far(sph[k], px[0], py[0], pz[0]);
-        if (!far) union_sdf<T, GRAD, 1>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
+        if constexpr (SCENE) scene_union<T, GRAD, 1>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
+        else if (!far) union_sdf<T, GRAD, 1>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
         finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
     }
 }
 
-template <typename T, int MAXA, bool GRAD>
+template <typename T, int MAXA, bool GRAD, bool SCENE = false>
 __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __restrict__ S,
                                           const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                           const CollArgs& a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                           T* __restrict__ dists, int64_t ldd, T* __restrict__ grads, int64_t ldg,
-                                          T* __restrict__ min_dist, const Tiling& tl, unsigned char* smem) {
+                                          T* __restrict__ min_dist, const Tiling& tl, unsigned char* smem,
+                                          const SceneArgs<T>& sa = SceneArgs<T>{}) {
     // gradient kernels: the union's KBox records into LDS (see kCollLdsBoxes); the launcher gives
     // the workgroup min(n_boxes, kCollLdsBoxes) * sizeof(KBox<T>) bytes
     const bool use_lds = GRAD && a.n_boxes <= kCollLdsBoxes;  // uniform
@@ -353,7 +472,9 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     else set_identity(f);
     const T trunc = (T)a.truncation;
     const T offs = (T)a.offset;
-    const bool broad = isfinite(a.truncation);  // uniform
+    const bool broad = !SCENE && isfinite(a.truncation);  // uniform (attached boxes: no union bound)
+    SceneCtx<T> sc;
+    if constexpr (SCENE) scene_frames(sc, sa, off);  // (plain SoA only: kin_coll_batch_scene)
     const T bnd[6] = {(T)a.bc[0], (T)a.bc[1], (T)a.bc[2], (T)a.bh[0], (T)a.bh[1], (T)a.bh[2]};
     T dmin = T(INFINITY);
     T ro[MAXA][3], rz[MAXA][3];
@@ -363,8 +484,9 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
         rz[s][0] = rz[s][1] = rz[s][2] = T(0);
     }
     const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
-    coll_spheres<T, MAXA, GRAD>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc, offs,
-                                broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds);
+    coll_spheres<T, MAXA, GRAD, SCENE>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
+                                       offs, broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds,
+                                       &sc);
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         step_a<T, KINHIP_COLL_FAST_TRIG != 0>(f, S[s], qa[s], ro[s], rz[s]);  // fp32 fast trig: see top
@@ -374,8 +496,9 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
             ro[s][1] = fma(rz[s][2], o0, -(rz[s][0] * o2));
             ro[s][2] = fma(rz[s][0], o1, -(rz[s][1] * o0));
         }
-        coll_spheres<T, MAXA, GRAD>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
-                                    offs, broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds);
+        coll_spheres<T, MAXA, GRAD, SCENE>(s, S[s].sph0, S[s].sph1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes,
+                                           trunc, offs, broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin,
+                                           smem, use_lds, &sc);
     }
     if (min_dist) {
         if (a.accumulate) dmin = fmin(dmin, ld_soa(min_dist, 0, 0, off));

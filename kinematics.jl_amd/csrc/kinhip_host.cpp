@@ -163,6 +163,12 @@ struct kin_model {
 
 struct kin_sdf {
     int device = -1;        // HIP device holding the box tables (current device at creation)
+    // boxes attached to a scene mechanism (kin_sdf_create_attached): group table + scene steps
+    bool attached = false;
+    int32_t n_groups = 0, scene_cols = 0, scene_base_col = -1;
+    void* d_scene_f32 = nullptr;  // KSceneGroup[n_groups], then KSceneStep<float>[] at scene_steps_off
+    void* d_scene_f64 = nullptr;
+    size_t scene_steps_off = 0;
     int32_t n_boxes = 0;
     int32_t n_aabb = 0;     // the first n_aabb boxes are axis-aligned (KAabb table after the KBox array)
     double bc[3] = {0, 0, 0}, bh[3] = {0, 0, 0};  // world-aligned box enclosing every box (broad phase, coll_body)
@@ -171,6 +177,8 @@ struct kin_sdf {
     ~kin_sdf() {
         if (d_f32) (void)hipFree(d_f32);
         if (d_f64) (void)hipFree(d_f64);
+        if (d_scene_f32) (void)hipFree(d_scene_f32);
+        if (d_scene_f64) (void)hipFree(d_scene_f64);
     }
 };
 
@@ -1198,6 +1206,170 @@ int kin_sdf_destroy(kin_sdf* s) {
     return KIN_OK;
 }
 
+int kin_sdf_create_attached(const kin_model* scene, int32_t n_q, const int32_t* q_joint_ids, int32_t n_boxes,
+                            const int32_t* link_ids, const double* origins16, const double* widths3, kin_sdf** out) {
+    auto bad = [](int code, const std::string& w) { return set_error(code, "kin_sdf_create_attached: " + w); };
+    if (!scene || !out || n_boxes < 1 || !link_ids || !origins16 || !widths3 || n_q < 0 || (n_q && !q_joint_ids))
+        return bad(KIN_E_INVALID, "null argument / no boxes");
+    const kin_model& m = *scene;
+    const int32_t J = m.n_joints(), L = m.n_links;
+    std::vector<int32_t> qcol(J, -1);
+    for (int32_t c = 0; c < n_q; ++c) {
+        const int32_t j = q_joint_ids[c] - 1;
+        if (j < 0 || j >= J) return bad(KIN_E_KEY, "scene joint id out of range");
+        if (m.jtype[j] != KIN_JOINT_FIXED) qcol[j] = c;
+    }
+    for (int32_t k = 0; k < 3 * n_boxes; ++k)
+        if (!(widths3[k] >= 0)) return bad(KIN_E_INVALID, "negative / NaN width");
+    // per box: the group (last batch joint on its root path, -1: the root / base frame) and its pose in
+    // the group frame (static joints at the scene's angles folded in, fp64, as joint_transform does)
+    struct BoxS { int32_t group; M34 pose; int32_t src; };
+    std::vector<BoxS> bs(n_boxes);
+    std::vector<int32_t> group_key;  // joint (0-based) or -1
+    for (int32_t k = 0; k < n_boxes; ++k) {
+        const int32_t l = link_ids[k] - 1;
+        if (l < 0 || l >= L) return bad(KIN_E_KEY, "box link id out of range");
+        std::vector<int32_t> path;  // joints root .. l
+        for (int32_t x = l; x >= 0 && m.link_pjoint[x] >= 0; x = m.plink(x)) path.push_back(m.link_pjoint[x]);
+        std::reverse(path.begin(), path.end());
+        int32_t last = -1;
+        for (size_t p = 0; p < path.size(); ++p)
+            if (qcol[path[p]] >= 0) last = (int32_t)p;
+        M34 S = m_identity();
+        for (size_t p = last + 1; p < path.size(); ++p) S = m_mul(S, m.joint_tf(path[p], m.angles[path[p]]));
+        const int32_t key = last >= 0 ? path[last] : -1;
+        auto it = std::find(group_key.begin(), group_key.end(), key);
+        if (it == group_key.end()) {
+            group_key.push_back(key);
+            it = group_key.end() - 1;
+        }
+        bs[k] = BoxS{(int32_t)(it - group_key.begin()), m_mul(S, m_from_col16(origins16 + 16 * k)), k};
+    }
+    if ((int)group_key.size() > kMaxSceneGroups)
+        return bad(KIN_E_UNSUPPORTED, "boxes ride on " + std::to_string(group_key.size()) + " moving frames (max " +
+                                          std::to_string(kMaxSceneGroups) + ")");
+    // group chains: static products up to each batch joint, then its motion (joint_transform)
+    std::vector<KSceneGroup> groups(group_key.size());
+    struct StepS { M34 F; double axis[3]; int32_t kind, qcol; };
+    std::vector<StepS> steps;
+    for (size_t g = 0; g < group_key.size(); ++g) {
+        groups[g].step0 = (int32_t)steps.size();
+        const int32_t key = group_key[g];
+        if (key >= 0) {
+            std::vector<int32_t> path;
+            for (int32_t x = m.jclink[key] - 1; x >= 0 && m.link_pjoint[x] >= 0; x = m.plink(x)) path.push_back(m.link_pjoint[x]);
+            std::reverse(path.begin(), path.end());
+            M34 S = m_identity();
+            for (int32_t j : path) {
+                if (qcol[j] >= 0) {
+                    StepS st;
+                    st.F = m_mul(S, m.pose(j));
+                    const double* ax = &m.jaxis[3 * j];
+                    const double nn = sqrt(ax[0] * ax[0] + ax[1] * ax[1] + ax[2] * ax[2]);
+                    for (int i = 0; i < 3; ++i) st.axis[i] = nn > 0 ? ax[i] / nn : 0.0;
+                    st.kind = m.jtype[j] == KIN_JOINT_PRISMATIC ? MOT_PRISM : MOT_REV;
+                    st.qcol = qcol[j];
+                    if (st.kind == MOT_PRISM) for (int i = 0; i < 3; ++i) st.axis[i] = ax[i];  // axis * q, unnormalised
+                    steps.push_back(st);
+                    S = m_identity();
+                } else {
+                    S = m_mul(S, m.joint_tf(j, m.angles[j]));
+                }
+            }
+        }
+        groups[g].step1 = (int32_t)steps.size();
+    }
+    // boxes sorted by group, axis-aligned ones first within a group
+    std::vector<int32_t> order;
+    std::vector<std::array<int, 3>> perms(n_boxes);
+    std::vector<char> aa(n_boxes, 0);
+    for (int32_t k = 0; k < n_boxes; ++k) {
+        double P16[16] = {0};
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) P16[i + 4 * j] = bs[k].pose.r[3 * i + j];
+            P16[12 + i] = bs[k].pose.t[i];
+        }
+        P16[15] = 1;
+        aa[k] = axis_permutation(P16, perms[k].data());
+    }
+    std::vector<KBox<float>> bf;
+    std::vector<KBox<double>> bd;
+    std::vector<KAabb<float>> af;
+    std::vector<KAabb<double>> ad;
+    for (size_t g = 0; g < groups.size(); ++g) {
+        groups[g].box0 = (int32_t)bf.size();
+        groups[g].aabb0 = (int32_t)af.size();
+        std::vector<int32_t> mem;
+        for (int32_t k = 0; k < n_boxes; ++k)
+            if (bs[k].group == (int32_t)g && aa[k]) mem.push_back(k);
+        groups[g].na = (int32_t)mem.size();
+        for (int32_t k = 0; k < n_boxes; ++k)
+            if (bs[k].group == (int32_t)g && !aa[k]) mem.push_back(k);
+        groups[g].nb = (int32_t)mem.size();
+        for (size_t o = 0; o < mem.size(); ++o) {
+            const int32_t k = mem[o];
+            const M34 inv = m_rigid_inverse(bs[k].pose);
+            KBox<float> xf{};
+            KBox<double> xd{};
+            to_row12<float>(inv, xf.inv);
+            to_row12<double>(inv, xd.inv);
+            for (int i = 0; i < 3; ++i) {
+                xf.half[i] = (float)(0.5 * widths3[3 * k + i]);
+                xd.half[i] = 0.5 * widths3[3 * k + i];
+            }
+            bf.push_back(xf);
+            bd.push_back(xd);
+            if ((int32_t)o < groups[g].na) {
+                KAabb<float> yf{};
+                KAabb<double> yd{};
+                for (int i = 0; i < 3; ++i) {
+                    const int j = perms[k][i];
+                    yd.c[i] = bs[k].pose.t[i];
+                    yf.c[i] = (float)bs[k].pose.t[i];
+                    yd.half[j] = 0.5 * widths3[3 * k + i];
+                    yf.half[j] = (float)(0.5 * widths3[3 * k + i]);
+                }
+                af.push_back(yf);
+                ad.push_back(yd);
+            }
+        }
+    }
+    auto sd = std::make_unique<kin_sdf>();
+    sd->attached = true;
+    sd->n_boxes = n_boxes;
+    sd->n_aabb = 0;
+    sd->n_groups = (int32_t)groups.size();
+    sd->scene_cols = n_q + (m.with_base ? 3 : 0);
+    sd->scene_base_col = m.with_base ? n_q : -1;
+    sd->scene_steps_off = ((sizeof(KSceneGroup) * groups.size() + 255) / 256) * 256;
+    auto upload_scene = [&](auto tag, void** dst) -> hipError_t {
+        using T = decltype(tag);
+        std::vector<KSceneStep<T>> hs(std::max<size_t>(1, steps.size()));
+        memset(hs.data(), 0, sizeof(KSceneStep<T>) * hs.size());
+        for (size_t k = 0; k < steps.size(); ++k) {
+            to_row12<T>(steps[k].F, hs[k].F);
+            for (int i = 0; i < 3; ++i) hs[k].axis[i] = (T)steps[k].axis[i];
+            hs[k].kind = steps[k].kind;
+            hs[k].qcol = steps[k].qcol;
+        }
+        const size_t nb = sd->scene_steps_off + sizeof(KSceneStep<T>) * hs.size();
+        hipError_t e = hipMalloc(dst, nb);
+        if (e == hipSuccess) e = hipMemcpy(*dst, groups.data(), sizeof(KSceneGroup) * groups.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy((char*)*dst + sd->scene_steps_off, hs.data(), sizeof(KSceneStep<T>) * hs.size(),
+                          hipMemcpyHostToDevice);
+        return e;
+    };
+    hipError_t e = hipGetDevice(&sd->device);
+    if (e == hipSuccess) e = upload_boxes(&sd->d_f32, bf, af);
+    if (e == hipSuccess) e = upload_boxes(&sd->d_f64, bd, ad);
+    if (e == hipSuccess) e = upload_scene(float(), &sd->d_scene_f32);
+    if (e == hipSuccess) e = upload_scene(double(), &sd->d_scene_f64);
+    if (e != hipSuccess) return bad(KIN_E_DEVICE, hipGetErrorString(e));
+    *out = sd.release();
+    return KIN_OK;
+}
+
 int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** out) {
     if (!m || !c || !out) return set_error(KIN_E_INVALID, "kin_coll_plan_create: null argument");
     if (c->n_spheres < 1 || !c->sphere_link_ids || !c->radii)
@@ -1300,6 +1472,7 @@ int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params
                       void* err, int64_t lde, void* stream) {
     if (!p || !sdf || !prm || !cp) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: null argument");
     if (!p->is_coll_ik) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: plan was not made by kin_coll_ik_plan_create");
+    if (sdf->attached) return set_error(KIN_E_UNSUPPORTED, "kin_ik_coll_batch: boxes attached to a scene mechanism");
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
     if (n == 0) return KIN_OK;
     if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
@@ -1366,6 +1539,7 @@ int coll_check(const kin_plan* p, const kin_sdf* sdf, const void* q, int64_t ldq
     auto bad = [&](const char* what) { return set_error(KIN_E_INVALID, std::string(fn) + ": " + what); };
     if (!p || !sdf) return bad("null plan / sdf");
     if (!p->is_coll) return bad("plan was not made by kin_coll_plan_create");
+    if (sdf->attached) return bad("the kin_sdf is attached to a scene: use kin_coll_batch_scene");
     if (n < 0) return bad("n < 0");
     if (n == 0) return KIN_OK;
     if (const int rc = check_device(p->device, fn, "the plan")) return rc;
@@ -1389,6 +1563,42 @@ int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, con
     if (rc != KIN_OK || n == 0) return rc;
     return coll_launch(p, sdf, coll_args(sdf, truncation, 0.0), q, ldq, n, dists, ldd, grads, ldg, min_dist, ta,
                        stream);
+}
+
+int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq,
+                         const void* scene_q, int64_t lds, int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg,
+                         void* min_dist, void* stream) {
+    auto bad = [](const std::string& w) { return set_error(KIN_E_INVALID, "kin_coll_batch_scene: " + w); };
+    if (!p || !sdf) return bad("null plan / sdf");
+    if (!p->is_coll) return bad("plan was not made by kin_coll_plan_create");
+    if (!sdf->attached) return bad("the kin_sdf is not attached to a scene (use kin_coll_batch)");
+    if (n < 0) return bad("n < 0");
+    if (n == 0) return KIN_OK;
+    if (sdf->scene_cols > 0 && (!scene_q || (lds != 0 && lds < n))) return bad("bad scene_q / lds");
+    if ((p->nqcols > 0 && (!q || ldq < n)) || (dists && ldd < n) || (grads && ldg < n)) return bad("bad pointer / stride");
+    if (const int rc = check_device(p->device, "kin_coll_batch_scene", "the plan")) return rc;
+    if (const int rc = check_device(sdf->device, "kin_coll_batch_scene", "the kin_sdf")) return rc;
+    CollArgs a = coll_args(sdf, truncation, 0.0);
+    const size_t np = p->parts.empty() ? 1 : p->parts.size();
+    for (size_t k = 0; k < np; ++k) {
+        const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
+        a.accumulate = k > 0;
+        const void* sc = s->dtype == KIN_F32 ? sdf->d_scene_f32 : sdf->d_scene_f64;
+        const SceneLaunch sl{sc, (const char*)sc + sdf->scene_steps_off, scene_q, lds, sdf->n_groups,
+                             sdf->scene_base_col, lds == 0 ? 1 : 0};
+        hipError_t e;
+        if (s->dtype == KIN_F32)
+            e = launch_coll_scene<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
+                                         (const KBox<float>*)sdf->d_f32, s->geom, a, sl, (const float*)q, ldq, n,
+                                         (float*)dists, ldd, (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
+        else
+            e = launch_coll_scene<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
+                                          (const KBox<double>*)sdf->d_f64, s->geom, a, sl, (const double*)q, ldq, n,
+                                          (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist,
+                                          (hipStream_t)stream);
+        if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll_scene launch: ") + hipGetErrorString(e));
+    }
+    return KIN_OK;
 }
 
 int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double truncation, int64_t tile, const void* q,

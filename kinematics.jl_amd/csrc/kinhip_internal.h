@@ -116,6 +116,19 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
                        int64_t ldd, T* grads, int64_t ldg, T* min_dist, const TileArgs& ta, const JitFns* jf,
                        hipStream_t st);
 
+// kin_coll_batch_scene: the scene side of k_coll_scene (device tables of the kin_sdf, scene columns)
+struct SceneLaunch {
+    const void* groups;  // KSceneGroup[ng]
+    const void* steps;   // KSceneStep<T>[]
+    const void* q;       // scene columns [cols][ld]
+    int64_t ld;
+    int32_t ng, base_col, uniform;
+};
+template <typename T>
+hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                             const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
+                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st);
+
 template <typename T>
 hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,
                                 int64_t ldv, hipStream_t st);

@@ -95,6 +95,30 @@ struct KAabb {
     T pad[2];
 };
 
+// Boxes attached to the links of a scene mechanism (kin_sdf_create_attached; src/sdf.jl:14-32,
+// 43-46, 82-97: UnionSDF(mech) follows get_transform of each box's link).  Boxes are grouped by the
+// scene's moving frame they ride on (the root / planar base, or the child frame of the last batch
+// joint on their path); static offsets down to the box are folded into the box records, which are in
+// the group frame.  A group's frame is the root (base) frame times its steps: F, then the joint's
+// motion about / along `axis` (kind MOT_REV / MOT_PRISM) by scene column qcol, or F alone (MOT_NONE).
+template <typename T>
+struct KSceneStep {
+    T F[12];    // row-major 3x4
+    T axis[3];  // unit joint axis
+    T pad;
+    int32_t kind;
+    int32_t qcol;
+    int32_t pad2[2];
+};
+struct KSceneGroup {
+    int32_t step0, step1;  // [step0, step1) of the KSceneStep array
+    int32_t box0;          // first box of the group in the KBox array (its KAabb entries at aabb0)
+    int32_t na, nb;        // axis-aligned boxes (first), all boxes
+    int32_t aabb0;
+    int32_t pad[2];
+};
+constexpr int kMaxSceneGroups = 4;  // moving frames carrying boxes (per-lane frames in registers)
+
 // kernel-side tiling: workgroup b works on tile b / tile_blocks (0xffffffff: plain SoA)
 struct Tiling {
     uint32_t tile_blocks;

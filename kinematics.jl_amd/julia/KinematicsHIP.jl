@@ -324,10 +324,23 @@ struct KinCollDesc
     radii::Ptr{Float64}
 end
 
-"""Device copy of a UnionSDF of BoxSDFs (or a single BoxSDF)."""
+struct KinIkCollParams
+    margin::Float64
+    band::Float64
+    weight::Float64
+    feas::Float64
+end
+
+"""Device copy of a UnionSDF of BoxSDFs (or a single BoxSDF); `n_scene_cols` > 0 (or `attached`):
+the boxes ride on a scene mechanism's links (kin_sdf_create_attached) and every batched call takes
+the scene columns."""
 mutable struct HIPSDF
     handle::Ptr{Cvoid}
+    attached::Bool
+    n_scene_cols::Int
+    scene::Union{Nothing,HIPModel}  # keeps the scene model alive
 end
+HIPSDF(h::Ptr{Cvoid}) = HIPSDF(h, false, 0, nothing)
 
 function HIPSDF(sdf::Kinematics.AbstractSDF)
     boxes = sdf isa Kinematics.UnionSDF ? sdf.sdfs : [sdf]
@@ -341,6 +354,30 @@ function HIPSDF(sdf::Kinematics.AbstractSDF)
     check(ccall((:kin_sdf_create_boxes, libkinhip), Cint, (Int32, Ptr{Float64}, Ptr{Float64}, Ref{Ptr{Cvoid}}),
                 length(boxes), poses, widths, h))
     s = HIPSDF(h[])
+    finalizer(x -> ccall((:kin_sdf_destroy, libkinhip), Cint, (Ptr{Cvoid},), x.handle), s)
+    s
+end
+
+"""UnionSDF(scene) (src/sdf.jl:82-97) that keeps following the scene: one box per link with box collision
+geometry, attached to that link (attach_to_link, :43-46); `joints` (+ the scene's base) are the scene
+columns of compute_coll_dists_and_grads!(...; scene_q) -- one value per column for the batch, or one
+column per configuration (e.g. a door-angle sweep)."""
+function HIPSDF(scene::Mechanism, joints::Vector{<:Joint})
+    links = [l for l in scene.links if l.geometric_meta_data isa Kinematics.BoxMetaData]
+    org = Float64[]
+    wid = Float64[]
+    for l in links
+        append!(org, vec(Matrix(l.geometric_meta_data.origin.mat)))
+        append!(wid, collect(l.geometric_meta_data.extents))
+    end
+    hm = HIPModel(scene; specialize=false)  # the scene's other joints at their current angles
+    jids = Int32[j.id for j in joints]
+    lids = Int32[l.id for l in links]
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:kin_sdf_create_attached, libkinhip), Cint,
+                (Ptr{Cvoid}, Int32, Ptr{Int32}, Int32, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ref{Ptr{Cvoid}}),
+                hm.handle, length(jids), jids, length(lids), lids, org, wid, h))
+    s = HIPSDF(h[], true, length(joints) + (scene.with_base ? 3 : 0), hm)
     finalizer(x -> ccall((:kin_sdf_destroy, libkinhip), Cint, (Ptr{Cvoid},), x.handle), s)
     s
 end
@@ -368,15 +405,73 @@ end
 function compute_coll_dists_and_grads!(hm::HIPModel, sscc::Kinematics.SweptSphereCollisionChecker,
                                        joints::Vector{<:Joint}, sdf::HIPSDF, Q::ROCMatrix{T},
                                        vals::ROCMatrix{T}, grads::Union{Nothing,ROCArray{T,3}};
-                                       truncation_dist=Inf) where {T}
+                                       truncation_dist=Inf, scene_q=nothing) where {T}
     N = size(Q, 1)
     p = coll_plan!(hm, T, sscc, joints)
+    if sdf.attached
+        scene_q === nothing && throw(ArgumentError("an attached HIPSDF needs scene_q"))
+        lds = scene_q isa ROCMatrix ? stride(scene_q, 2) : 0  # (N, cols) per configuration, or one vector
+        check(ccall((:kin_coll_batch_scene, libkinhip), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Float64, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64,
+                     Ptr{T}, Ptr{Cvoid}),
+                    p, sdf.handle, truncation_dist, pointer(Q), stride(Q, 2), pointer(scene_q), lds, N, pointer(vals),
+                    N, grads === nothing ? C_NULL : pointer(grads), N, C_NULL, stream_ptr()))
+        return vals, grads
+    end
     check(ccall((:kin_coll_batch, libkinhip), Cint,
                 (Ptr{Cvoid}, Ptr{Cvoid}, Float64, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{T},
                  Ptr{Cvoid}),
                 p, sdf.handle, truncation_dist, pointer(Q), stride(Q, 2), N, pointer(vals), N,
                 grads === nothing ? C_NULL : pointer(grads), N, C_NULL, stream_ptr()))
     vals, grads
+end
+
+"""Batched collision-aware IK, inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
+(src/inverse_kinematics.jl:1-21) for every row of `targets` (N, 12): stage 1 the collision-free DLS
+(kin_ik_dls_batch_from, seeds Q0), stage 2 kin_ik_coll_batch (the IneqConst(sscc, joints, sdf, 1, margin)
+sphere rows), both on one plan of kin_coll_ik_plan_create.  Returns (Q, iters, err (N, 3))."""
+function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
+                                        Q0::ROCMatrix{T}, sscc::Kinematics.SweptSphereCollisionChecker, sdf::HIPSDF;
+                                        use_bistage=true, margin=0.02, band=0.0, weight=1.0, feas=1e-6,
+                                        max_iters=64, lambda=1e-2, tol_pos=1e-3, tol_rot=1e-3, max_step=0.5,
+                                        rpy_objective=true, restarts=3, seed=0, index_base=0) where {T}
+    N = size(Q0, 1)
+    ids = Int32[j.id for j in joints]
+    sph = Int32[l.id for l in sscc.sphere_links]
+    key = (:collik, T, ids, sph, link.id)
+    p = cached_plan!(hm, key, ids) do
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        r = Float64.(sscc.sphere_radii)
+        GC.@preserve ids sph r begin
+            d = KinCollDesc(dtype_code(T), length(ids), pointer(ids), length(sph), pointer(sph), C_NULL, pointer(r))
+            check(ccall((:kin_coll_ik_plan_create, libkinhip), Cint,
+                        (Ptr{Cvoid}, Ref{KinCollDesc}, Int32, Ref{Ptr{Cvoid}}), hm.handle, d, Int32(link.id), h))
+        end
+        hm.specialize && ccall((:kin_plan_specialize, libkinhip), Cint, (Ptr{Cvoid}, UInt32), h[], UInt32(0))
+        h[]
+    end
+    Q1 = similar(Q0)
+    Q = similar(Q0)
+    iters = ROCVector{Int32}(undef, N)
+    err = ROCMatrix{T}(undef, N, 3)
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, rpy_objective ? 2 : 1, restarts, seed, 0,
+                      index_base)
+    if use_bistage
+        check(ccall((:kin_ik_dls_batch_from, libkinhip), Cint,
+                    (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T},
+                     Int64, Ptr{Cvoid}),
+                    p, prm, pointer(targets), stride(targets, 2), pointer(Q0), pointer(Q1), stride(Q1, 2), N,
+                    pointer(iters), pointer(err), N, stream_ptr()))
+    else
+        copyto!(Q1, Q0)
+    end
+    cprm = KinIkCollParams(margin, band, weight, feas)
+    check(ccall((:kin_ik_coll_batch, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64,
+                 Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),
+                p, sdf.handle, prm, cprm, pointer(targets), stride(targets, 2), pointer(Q1), pointer(Q), stride(Q, 2),
+                N, pointer(iters), pointer(err), N, stream_ptr()))
+    Q, iters, err
 end
 
 """IneqConst over every waypoint column of Xi (N = waypoints of one or many trajectories, rows = dof):

@@ -15,7 +15,7 @@ from .mechanism import (  # noqa: F401
 )
 from .synth import uniform_configs  # noqa: F401
 from .collision import (  # noqa: F401
-    FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, BoxSDF, CollisionIKPlan, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
+    FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, AttachedUnionSDF, BoxSDF, CollisionIKPlan, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
     add_coll_links, add_fetch_arm_spheres, compute_coll_dists, compute_coll_dists_, compute_coll_dists_and_grads,
     compute_coll_dists_and_grads_, compute_swept_sphere, fridge_sdf,
 )

@@ -72,6 +72,38 @@ class UnionSDF:
         return min(b(p) for b in self.sdfs)
 
 
+class AttachedUnionSDF:
+    """``UnionSDF(mech)`` (src/sdf.jl:82-97) that keeps following the scene mechanism: one BoxSDF per link
+    with box collision geometry, attached to that link (attach_to_link, :43-46), its world pose
+    get_transform(scene, link) * origin (:14-32) evaluated on the device for every sample
+    (kin_sdf_create_attached).  `joints` (+ the scene's planar base when it has with_base) are the scene
+    columns of ``CollisionPlan.run(..., scene_q=...)``: one column vector for the whole batch, or one per
+    sample (e.g. a door-angle sweep in one launch).  Other scene joints stay at the scene's current angles."""
+
+    def __init__(self, scene: Mechanism, joints=()):
+        scene._sync_angles()
+        links = [l for l in scene.links if l.geometric_meta_data is not None and hasattr(l.geometric_meta_data, "extents")]
+        if not links:
+            raise ValueError("AttachedUnionSDF: the scene has no box collision geometry")
+        self.scene, self.joints = scene, list(joints)
+        self.links = links
+        jids = _i32([j.id for j in self.joints])
+        lids = _i32([l.id for l in links])
+        org = np.ascontiguousarray(np.array([np.asarray(l.geometric_meta_data.origin, np.float64).T.reshape(16)
+                                             for l in links]).reshape(-1))
+        wid = np.ascontiguousarray(np.array([l.geometric_meta_data.extents for l in links], np.float64).reshape(-1))
+        self.n_scene_cols = len(self.joints) + (3 if scene.with_base else 0)
+        self._h = C.c_void_p()
+        K.check(K.lib().kin_sdf_create_attached(scene._model, jids.size, _p(jids) if jids.size else None, lids.size,
+                                                _p(lids), _p(org), _p(wid), C.byref(self._h)))
+        self.device_index = _current_device_index()
+
+    def __del__(self):
+        if getattr(self, "_h", None) and K._lib is not None:
+            K._lib.kin_sdf_destroy(self._h)
+            self._h = None
+
+
 class SweptSphereCollisionChecker:
     """src/collision.jl:32-49: spheres are fixed child links of the mechanism's links."""
 
@@ -147,9 +179,13 @@ class CollisionPlan:
         return D, G, Mn
 
     def run(self, sdf: UnionSDF, Q: torch.Tensor, dists=True, grads=False, min_dist=False,
-            truncation=float("inf"), stream=None):
+            truncation=float("inf"), stream=None, scene_q: Optional[torch.Tensor] = None):
         """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async.
-        `dists` / `grads` may also be preallocated (row-padded) output views of those shapes."""
+        `dists` / `grads` may also be preallocated (row-padded) output views of those shapes.
+        With an ``AttachedUnionSDF``: `scene_q` = its scene columns, (n_scene_cols, N) per sample or
+        (n_scene_cols,) for the whole batch (kin_coll_batch_scene)."""
+        if isinstance(sdf, AttachedUnionSDF):
+            return self._run_scene(sdf, Q, dists, grads, min_dist, truncation, stream, scene_q)
         if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
         N = Q.shape[1]
@@ -171,6 +207,40 @@ class CollisionPlan:
         K.check(K.lib().kin_coll_batch(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0), N, ptr(D), ldd,
                                        ptr(G), ldg, ptr(Mn), st))
         return D, G, Mn
+
+
+def _run_scene(self, sdf, Q, dists, grads, min_dist, truncation, stream, scene_q):
+    if Q.dtype != self.dtype or not Q.is_cuda or Q.dim() != 2 or Q.shape[0] != self.n_dof or Q.stride(1) != 1:
+        raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_dof}, N)")
+    N = Q.shape[1]
+    _plan_device(self, Q)
+    _plan_device(sdf, Q)
+    if scene_q is None:
+        raise ValueError("an AttachedUnionSDF needs scene_q (its scene joint values)")
+    if scene_q.dtype != self.dtype:
+        raise ValueError("scene_q must have the plan dtype")
+    _same_device(scene_q, Q, "scene_q")
+    if scene_q.dim() == 1:
+        if scene_q.shape[0] != sdf.n_scene_cols or not scene_q.is_contiguous():
+            raise ValueError(f"scene_q must hold {sdf.n_scene_cols} values")
+        lds = 0
+    else:
+        if scene_q.shape != (sdf.n_scene_cols, N) or scene_q.stride(1) != 1:
+            raise ValueError(f"scene_q must be ({sdf.n_scene_cols}, N) with unit sample stride")
+        lds = scene_q.stride(0)
+    dev = Q.device
+    D = torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None
+    G = torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None
+    Mn = torch.empty(N, dtype=self.dtype, device=dev) if min_dist else None
+    st = (stream or torch.cuda.current_stream(dev)).cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None
+    K.check(K.lib().kin_coll_batch_scene(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0),
+                                         scene_q.data_ptr() if scene_q.numel() else None, lds, N, ptr(D), N, ptr(G),
+                                         N, ptr(Mn), st))
+    return D, G, Mn
+
+
+CollisionPlan._run_scene = _run_scene
 
 
 class CollisionIKPlan(Plan):

@@ -102,6 +102,7 @@ def _assert_mismatches_at_kinks(om, box, Q, ids, sph, rad, g_gpu, g_ref, gtol, h
     and to the left disagree by more than gtol (a box kink -- union argmin switch, inside medial plane,
     the surface -- or the edge region within ~1e-3 of a box where eps-sized differences lose the
     derivative).  Returns the number of such entries."""
+    gtol = np.broadcast_to(np.asarray(gtol, np.float64), g_gpu.shape)  # scalar or per entry
     bad = np.argwhere(np.abs(g_gpu - g_ref) > gtol)  # (sphere k, dof i, config n)
     if bad.size == 0:
         return 0
@@ -118,7 +119,7 @@ def _assert_mismatches_at_kinks(om, box, Q, ids, sph, rad, g_gpu, g_ref, gtol, h
     for j, (k, i, n) in enumerate(bad):
         right = (d_pm[k, 2 * j] - d0[k, j]) / h
         left = (d0[k, j] - d_pm[k, 2 * j + 1]) / h
-        assert abs(right - left) > gtol, (k, i, n, right, left, g_gpu[k, i, n], g_ref[k, i, n])
+        assert abs(right - left) > gtol[k, i, n], (k, i, n, right, left, g_gpu[k, i, n], g_ref[k, i, n])
     return len(bad)
 
 
@@ -322,7 +323,10 @@ def test_gpu_collision_multi_chain(dtype):
     np.testing.assert_allclose(D.double().cpu().numpy(), rd, atol=tol)
     np.testing.assert_allclose(Mn.double().cpu().numpy(), rd.min(0), atol=tol)
     gd = G.double().cpu().numpy()
-    assert (np.abs(gd - rg) > (2e-5 if dtype == torch.float64 else 1e-4)).mean() < 1e-3
+    # analytic vs the reference's forward difference: every disagreement sits at a kink (VERDICT r02:
+    # no blanket outlier allowance)
+    _assert_mismatches_at_kinks(om, O.OracleUnionSDF(poses, widths), Q.double().cpu().numpy(), ids, sph, rad, gd, rg,
+                                2e-5 if dtype == torch.float64 else 1e-4, h=1e-7 if dtype == torch.float64 else 1e-5)
     assert not np.any(gd[:14, 8:]) and not np.any(gd[14:, 1:8])  # arm spheres vs head joints and vice versa
     V, Jv = kinhip.IneqConst(sscc, joints, sdf, 1, 0.03, dtype=dtype).eval_batch(Q)
     np.testing.assert_allclose(V.double().cpu().numpy(), np.minimum(rd, 0.08) - 0.03, atol=tol)
@@ -445,3 +449,67 @@ def test_gpu_collision_launch_chunk_boundary():
     ids = [tree.joint_id(n) for n in ARM]
     rd, _ = O.coll_batch(om, O.OracleUnionSDF(poses, widths), Q[:, idx].double().cpu().numpy(), ids, sph, rad)
     np.testing.assert_allclose(Mn[idx].double().cpu().numpy(), rd.min(0), atol=2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gpu_attached_scene_door_sweep(dtype):
+    """VERDICT r02 #6, src/sdf.jl:14-32, 43-46, 82-97: UnionSDF(fridge) with its boxes attached to the
+    fridge's links follows door_joint and the fridge's planar base.  One launch sweeps 8 door angles
+    (and, for half of the samples, base poses): every sample's distances / minimum / gradients vs the
+    oracle's UnionSDF built at that sample's scene state (fp64 1e-9, fp32 1e-6); a launch with one
+    scene state for the whole batch equals the static kin_sdf_create_boxes union of that state."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    door = fr.find_joint("door_joint")
+    sdf = kinhip.AttachedUnionSDF(fr, [door])
+    assert sdf.n_scene_cols == 4
+    angles = np.linspace(0.0, 2.4, 8)
+    per = 400
+    N = per * len(angles)
+    rng = np.random.default_rng(31)
+    sq = np.zeros((4, N))
+    for a_i, a in enumerate(angles):
+        sl = slice(a_i * per, (a_i + 1) * per)
+        sq[0, sl] = a
+        sq[1, sl], sq[2, sl], sq[3, sl] = 1.2, 0.0, 0.0
+        half = slice(a_i * per + per // 2, (a_i + 1) * per)  # moved / turned fridges
+        sq[1, half] = 1.15 + 0.1 * (a_i % 3)
+        sq[2, half] = -0.05 * (a_i % 2)
+        sq[3, half] = 0.15 * ((a_i % 4) - 1.5)
+    g = torch.Generator().manual_seed(7)
+    Q = (torch.rand((8, N), generator=g, dtype=torch.float64) * 2.4 - 1.2).to(dtype).to(dev)
+    SQ = torch.tensor(sq, dtype=dtype, device=dev).contiguous()
+    plan = sscc.plan(arm, dtype=dtype)
+    D, G, Mn = plan.run(sdf, Q, grads=True, min_dist=True, scene_q=SQ)
+    tree, om, sph, rad = _fetch_with_spheres(False)
+    ids = [tree.joint_id(n) for n in ARM]
+    fr_tree = O.parse_urdf_tree(golden("fridge.urdf"))
+    tol = 1e-9 if dtype == torch.float64 else 1e-6
+    qd = Q.double().cpu().numpy()
+    sqd = SQ.double().cpu().numpy()  # the scene values as the kernel saw them
+    states = {}
+    for k in range(N):
+        states.setdefault(tuple(sqd[:, k]), []).append(k)
+    for st, cols in states.items():
+        poses, widths = O.fridge_boxes(fr_tree, door_angle=st[0], base=st[1:])
+        box = O.OracleUnionSDF(poses, widths)
+        rd, rg = O.coll_batch(om, box, qd[:, cols], ids, sph, rad)
+        np.testing.assert_allclose(D.double().cpu().numpy()[:, cols], rd, atol=tol)
+        np.testing.assert_allclose(Mn.double().cpu().numpy()[cols], rd.min(0), atol=tol)
+        _assert_mismatches_at_kinks(om, box, qd[:, cols], ids, sph, rad, G.double().cpu().numpy()[:, :, cols], rg,
+                                    2e-5 if dtype == torch.float64 else 1e-4, h=1e-7 if dtype == torch.float64 else 1e-5)
+    # one scene state for the whole launch (lds = 0) == the static union of that state
+    st = torch.tensor([2.0, 1.2, 0.0, 0.0], dtype=dtype, device=dev)
+    D1, G1, M1 = plan.run(sdf, Q, grads=True, min_dist=True, scene_q=st)
+    D2, G2, M2 = plan.run(kinhip.fridge_sdf(fr, 2.0, (1.2, 0.0, 0.0)), Q, grads=True, min_dist=True)
+    torch.testing.assert_close(D1, D2, atol=tol, rtol=0)
+    torch.testing.assert_close(M1, M2, atol=tol, rtol=0)
+    assert float((G1 - G2).abs().gt(1e-4).float().mean()) < 1e-3  # (argmin ties between the two box orders)
+    with pytest.raises(ValueError):
+        plan.run(sdf, Q, min_dist=True)  # scene values are required
+    with pytest.raises(kinhip.KinError):
+        kinhip._lib.check(kinhip._lib.lib().kin_coll_batch(plan._h, sdf._h, 1.0, Q.data_ptr(), Q.stride(0), N, None, N,
+                                                           None, N, M1.data_ptr(), None))

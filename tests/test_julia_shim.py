@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "kinhip.h")
 SHIM = os.path.join(ROOT, "kinematics.jl_amd", "julia", "KinematicsHIP.jl")
 
 STRUCTS = {"KinTreeDesc": "kin_tree_desc", "KinPlanDesc": "kin_plan_desc", "KinIkParams": "kin_ik_params",
-           "KinCollDesc": "kin_coll_desc"}
+           "KinCollDesc": "kin_coll_desc", "KinIkCollParams": "kin_ik_coll_params"}
 
 
 def _strip_c_comments(s):
@@ -124,7 +124,8 @@ def test_julia_struct_mirrors_c_struct(jl_name):
 
 
 RUN_ENTRIES = ("kin_plan_run", "kin_plan_run_tiled", "kin_ik_dls_batch", "kin_ik_dls_batch_from",
-               "kin_point_ik_nakamura_batch", "kin_coll_batch", "kin_ineq_const_batch", "kin_pose_const_batch")
+               "kin_point_ik_nakamura_batch", "kin_coll_batch", "kin_ineq_const_batch", "kin_pose_const_batch",
+               "kin_coll_batch_scene", "kin_ik_coll_batch")
 
 
 def jl_functions(src):
@@ -148,7 +149,7 @@ def test_every_cached_plan_path_goes_through_the_staleness_check():
             for entry in RUN_ENTRIES:
                 if re.search(r"ccall\(\(:%s,\s*libkinhip\)" % entry, body):
                     runners += 1
-                    assert re.search(r"\b(plan!|coll_plan!)\(hm,", body), (name, entry)
+                    assert re.search(r"\b(plan!|coll_plan!|cached_plan!)\(hm,", body), (name, entry)
     assert runners >= 9
     for name in ("plan!", "coll_plan!"):
         (body,) = fns[name]
