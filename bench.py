@@ -264,6 +264,13 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
             out[name]["margin"] = 0.03
         if name.endswith("tiled"):
             out[name]["layout"] = f"tiled SoA, tile {tile}"
+    # ceilings of the distances + gradients legs (8 rows in, 14 + 112 rows out) from the same run
+    for name, tl_ in (("dists_grads", 0), ("dists_grads_tiled", tile)):
+        pat_c = _pattern_us(8, ns + ns * 8, n, tl_, stream)
+        out[name]["pattern_ceiling_us"] = pat_c
+        out[name]["frac_of_pattern"] = pat_c / out[name]["avg_launch_us"]
+        out[name]["frac"] = out[name]["achieved_GBs"] / HBM_PEAK_GBS
+    out["tiled_vs_plain_dists_grads"] = out["dists_grads"]["avg_launch_us"] / out["dists_grads_tiled"]["avg_launch_us"]
     out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
                        f"samples sharded across ranks, {'specialised' if spec else 'generic'} kernels")
     return out
@@ -404,6 +411,41 @@ def _pmc_traffic(workload, fname="pmc_fk_jac_f32.json"):
     return None
 
 
+_PROBE = None
+
+
+def _pattern_us(rows_in, rows_out, n, tile, stream, reps=20, warmup=3):
+    """The access pattern of a leg with no arithmetic (kinematics.jl_amd/lib/libkinprobe.so, a measurement
+    probe built beside the engine): rows_in rows of q read and rows_out rows written per configuration,
+    fp32, tiled SoA (tile > 0) or plain rows (tile = 0), non-temporal stores like k_fk / k_coll.  Average
+    launch time (µs) from HIP events on `stream`: the leg's ceiling measured in the same run."""
+    global _PROBE
+    import ctypes as C
+    if _PROBE is None:
+        _PROBE = C.CDLL(os.path.join(ROOT, "kinematics.jl_amd", "lib", "libkinprobe.so"))
+        _PROBE.kinprobe_pattern.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+        _PROBE.kinprobe_pattern.restype = C.c_int
+    ntot = -(-n // tile) * tile if tile else n
+    q = torch.zeros(rows_in * ntot, dtype=torch.float32, device=stream.device)
+    out = torch.zeros(rows_out * ntot, dtype=torch.float32, device=stream.device)
+    st = stream.cuda_stream
+
+    def launch():
+        rc = _PROBE.kinprobe_pattern(rows_in, rows_out, n, tile, q.data_ptr(), out.data_ptr(), st)
+        assert rc == 0, rc
+    for _ in range(warmup):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    del q, out
+    return us
+
+
 def _cold_leg(leg, n, stream, bytes_per_eval, reps=10):
     """One launch at a time after a 1 GiB read (torch sum) has evicted the Infinity Cache: the
     launch's own HIP events bracket it alone (the read is outside them)."""
@@ -536,6 +578,11 @@ def main():
                                          "profiles" if traffic else None)
     if args.extras:
         out["roofline"]["torch_copy_GBs"] = _copy_bw(dev)  # context: torch device-to-device copy rate
+        # the same bytes in the same layout with no kinematics (8 rows read, 60 written): this leg's ceiling
+        pat = _pattern_us(8, 60, N, args.tile if args.layout == "tiled" else 0, stream)
+        out["roofline"]["pattern_ceiling"] = {"avg_launch_us": pat, "frac_of_pattern": pat / (t_launch * 1e6),
+                                              "achieved_GBs": bytes_per_eval * N / pat / 1e3,
+                                              "probe": "kinprobe_pattern(8 in, 60 out, same layout), same run"}
         # The 2^20 working set (q + outputs, 285 MB) is about the 256 MiB Infinity Cache, so back-to-back
         # launches find part of the previous launch's lines on die.  Two checks beside the headline:
         # the same launch after a 1 GiB read has evicted the cache (cold), and batches 4x and 16x the
@@ -547,8 +594,10 @@ def main():
             for lg, k_s in ((22, 10), (24, 5)):
                 w_b, d_b = timed_leg(torch.float32, True, [gl], args.layout, n=1 << lg, steps=k_s, warmup=2)
                 ach = bytes_per_eval * (1 << lg) / (d_b / k_s) / 1e9
+                pat_b = _pattern_us(8, 60, 1 << lg, args.tile, stream, reps=k_s, warmup=1)
                 big[f"2^{lg}"] = {"evals_per_s": (1 << lg) * ws * k_s / w_b, "avg_launch_us": d_b / k_s * 1e6,
                                   "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                                  "pattern_ceiling_us": pat_b, "frac_of_pattern": pat_b / (d_b / k_s * 1e6),
                                   "working_set_MB": bytes_per_eval * (1 << lg) / 1e6,
                                   "kernel": ("kinhip_jit_fks (grid-strided, 2 configurations per lane)"
                                              if lg >= 23 and args.spec else "as the headline")}

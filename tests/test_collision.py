@@ -244,7 +244,10 @@ def test_gpu_collision_lds_box_limit(n_boxes):
     spe = sscc.plan(arm, dtype=torch.float32).specialize()
     D0, G0, M0 = gen.run(sdf, Q, grads=True, min_dist=True)
     D1, G1, M1 = spe.run(sdf, Q, grads=True, min_dist=True)
-    assert torch.equal(D0, D1) and torch.equal(G0, G1) and torch.equal(M0, M1)
+    # distances and minima bit-equal; gradients to a few ulp (the two compilations contract the
+    # argmin box's gradient product-sums differently; measured <= 3e-7, tools/coll_spec_diff.py)
+    assert torch.equal(D0, D1) and torch.equal(M0, M1)
+    torch.testing.assert_close(G0, G1, atol=1e-6, rtol=0)
     tree, om, sph, rad = _fetch_with_spheres(False)
     box = O.OracleUnionSDF(poses, widths)
     ids = [tree.joint_id(n) for n in ARM]
@@ -351,18 +354,22 @@ def test_gpu_collision_specialized_equals_generic(dtype, with_base):
     gen = sscc.plan(arm, dtype=dtype)
     spe = sscc.plan(arm, dtype=dtype).specialize()
     assert spe.specialized == kinhip.KIN_SPEC_COLL
+    gtol = 1e-6 if dtype == torch.float32 else 1e-15  # gradients: a few ulp (see test_gpu_collision_lds_box_limit)
     for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True),
                dict(dists=True, grads=True, truncation=0.1)):
-        for x, y in zip(gen.run(sdf, Q, **kw), spe.run(sdf, Q, **kw)):
-            assert (x is None and y is None) or torch.equal(x, y), kw
+        for k, (x, y) in enumerate(zip(gen.run(sdf, Q, **kw), spe.run(sdf, Q, **kw))):
+            if k == 1 and x is not None:
+                torch.testing.assert_close(x, y, atol=gtol, rtol=0)
+            else:
+                assert (x is None and y is None) or torch.equal(x, y), kw
     if not with_base:  # two chains (arm + head)
         sscc.add_coll_sphere(m.find_link("head_pan_link"), (0.05, 0.0, 0.1), 0.12)
         joints = arm + [m.find_joint("head_pan_joint"), m.find_joint("head_tilt_joint")]
         Q2 = (torch.rand((10, N), generator=g, dtype=torch.float64) * 2 - 1).to(dtype).to(dev)
         a = sscc.plan(joints, dtype=dtype).run(sdf, Q2, grads=True, min_dist=True)
         b = sscc.plan(joints, dtype=dtype).specialize().run(sdf, Q2, grads=True, min_dist=True)
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+        torch.testing.assert_close(a[1], b[1], atol=1e-6 if dtype == torch.float32 else 1e-15, rtol=0)
 
 
 @pytest.mark.gpu
