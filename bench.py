@@ -390,8 +390,12 @@ def _copy_bw(dev, nbytes=1 << 31):
 def _pmc_valu(fname):
     """Issue-based VALU busy of a committed PMC summary (tools/summarize_prof.py), for the legs whose
     bound is VALU / latency rather than HBM (configs 4 and 5)."""
-    p = os.path.join(ROOT, "profiles", fname)
-    if not os.path.exists(p):
+    for rnd in ("r03_", "r02_"):  # the newest committed round's summary
+        p = os.path.join(ROOT, "profiles", rnd + fname)
+        if os.path.exists(p):
+            fname = rnd + fname
+            break
+    else:
         return None
     with open(p) as f:
         d = json.load(f)
@@ -664,13 +668,13 @@ def main():
         out["config2_fk6_f64"] = {"value": N * ws * k2 / w2, "unit": "evals/s", "avg_launch_us": d2 / k2 * 1e6,
                                   "achieved_GBs": (8 + 72) * 8 * N / (d2 / k2) / 1e9, "layout": lay64}
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec)
-        out["config4_ik_dls"]["pmc"] = _pmc_valu("r02_pmc_ik32s.json")
+        out["config4_ik_dls"]["pmc"] = _pmc_valu("pmc_ik32s.json")
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
         out["config4_ik_dls_f64"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, dt=torch.float64)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec)
-        out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("r02_pmc_coll32s.json")
-        out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("r02_pmc_collg32s.json")
-        out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("r02_pmc_collg32ts.json")
+        out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("pmc_coll32s.json")
+        out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("pmc_collg32s.json")
+        out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("pmc_collg32ts.json")
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
         if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)
             out["generic_kernels"] = {

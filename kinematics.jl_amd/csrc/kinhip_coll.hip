@@ -45,7 +45,7 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
         sa.groups = (const KSceneGroup*)sl.groups;
         sa.steps = (const KSceneStep<T>*)sl.steps;
         sa.q = (const T*)sl.q + (sl.uniform ? 0 : s0);
-        sa.ld = sl.ld;
+        sa.ld = sl.uniform ? 1 : sl.ld;  // uniform: the scene values are one column of cols entries
         sa.ng = sl.ng;
         sa.base_col = sl.base_col;
         sa.uniform = sl.uniform;

@@ -99,18 +99,22 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
     for (int i = 0; i < NS; ++i) {
         d[i] = signed_sqrt(best[i]);
         if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
+            // explicit address spaces: the two gathers are ds_read and global_load, never one flat
+            // load through a selected pointer (which the optimiser otherwise forms from the branch)
             KBox<T> b;
             if (use_lds) {
-                const KBox<T>* lb = reinterpret_cast<const KBox<T>*>(smem);
+                const __attribute__((address_space(3))) KBox<T>* lb =
+                    (const __attribute__((address_space(3))) KBox<T>*)smem;
 #pragma unroll
                 for (int j = 0; j < 12; ++j) b.inv[j] = lb[bk[i]].inv[j];
 #pragma unroll
                 for (int j = 0; j < 3; ++j) b.half[j] = lb[bk[i]].half[j];
             } else {
+                const __attribute__((address_space(1))) KBox<T>* gb = (const __attribute__((address_space(1))) KBox<T>*)boxes;
 #pragma unroll
-                for (int j = 0; j < 12; ++j) b.inv[j] = boxes[bk[i]].inv[j];
+                for (int j = 0; j < 12; ++j) b.inv[j] = gb[bk[i]].inv[j];
 #pragma unroll
-                for (int j = 0; j < 3; ++j) b.half[j] = boxes[bk[i]].half[j];
+                for (int j = 0; j < 3; ++j) b.half[j] = gb[bk[i]].half[j];
             }
             T l[3], q[3], gl[3];
 #pragma unroll
@@ -142,7 +146,7 @@ struct SceneArgs {
     const KSceneGroup* groups = nullptr;
     const KSceneStep<T>* steps = nullptr;
     const T* q = nullptr;    // scene columns [cols][ld] (per sample), or one sample for the whole launch
-    int64_t ld = 0;
+    int64_t ld = 0;          // uniform: 1 (q[col])
     int32_t ng = 0;
     int32_t base_col = -1;   // scene planar base (x, y, theta) columns, -1: none
     int32_t uniform = 0;     // 1: every sample uses the scene column values of sample 0

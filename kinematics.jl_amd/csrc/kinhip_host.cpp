@@ -1685,7 +1685,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     // that schedule touches it, so every other call stays allocation-free (capture-safe)
     IkScratch scr;
     if (ik_wants_two_phase(a, n, kin_plan::kIkScratchCap)) {
-        const size_t set_bytes = sizeof(int32_t) * kin_plan::kIkScratchCap + 256;
+        const size_t set_bytes = 2 * sizeof(int32_t) * kin_plan::kIkScratchCap + 256;  // ring + aux ring
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
         const bool capturing = cs == hipStreamCaptureStatusActive;
@@ -1715,6 +1715,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
             unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * set;
             scr.fail_ctl = (uint32_t*)base;
             scr.fail_list = (int32_t*)(base + 256);
+            scr.fail_aux = scr.fail_list + kin_plan::kIkScratchCap;
             scr.cap = kin_plan::kIkScratchCap;
         }
     }

@@ -95,6 +95,18 @@ bool ik_wants_two_phase(const IkArgs& a, int64_t n, int64_t cap) {
     return false;
 }
 
+// Phase-1 hand-over point (IkArgsT::p1_cut): 5/8 of an attempt by default.  Config 4 (L = 16):
+// 23% of the targets are still unsolved after 10 iterations (46% after 8, 4% after 16; oracle
+// histogram), so phase 2 keeps about one wave per SIMD; measured 0.081 ms vs 0.089 (no hand-over),
+// 0.092 (cut 8), 0.084 (cut 12) fp32 and 0.165 / 0.179 / 0.236 / 0.170 ms fp64
+// (profiles/r03_ik_handover.txt).  KINHIP_IK_P1_CUT=<iterations> overrides (A/B build; 0 disables).
+// 0 when the hand-over is not allowed or not shorter than L.
+static int ik_p1_cut(int L, bool allowed) {
+    static const int env = ab_env_int("KINHIP_IK_P1_CUT", -1);
+    const int cut = env >= 0 ? env : (5 * L) / 8;
+    return allowed && cut > 0 && cut < L ? cut : 0;
+}
+
 thread_local bool g_ik_partial = false;
 bool ik_last_call_partial() { return g_ik_partial; }
 
@@ -173,6 +185,15 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a1.fail_list = scr.fail_list;
             a1.fail_ctl = scr.fail_ctl;
             a1.fail_mask = (uint32_t)(scr.cap - 1);
+            a1.fail_aux = scr.fail_aux;
+            // early hand-over (IkArgsT::p1_cut): attempt 0 stops after `cut` iterations in phase 1 and
+            // phase 2 resumes it on slot 0 beside the other attempts.  Phase 1 then lasts `cut`
+            // iterations instead of L and phase 2 (16 targets per wave at G = 4) absorbs the handed-over
+            // ones at no extra latency while it stays within ~2 waves per SIMD (one wave alone issues
+            // every other VALU slot).  Not for in-place calls of based plans (the hand-over would
+            // overwrite the start pose that attempts 1, 2, ... begin from).
+            const int cut = ik_p1_cut(L, P.flags & PF_BASE ? (q0 != nullptr) : true);
+            a1.p1_cut = cut;
             // phase 1 shares out targets like the one-phase schedule (one per lane while the batch
             // fills the chip in at most two rounds of waves, else wave-local queues) -- but a queue
             // of `resident_waves` waves must not run fewer waves per CU than the kernel could hold:
@@ -190,12 +211,16 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             const int64_t w1 = q1 ? std::min(resident_waves, plain1) : plain1;
             const int64_t pw1 = (c + w1 - 1) / w1;
             if ((e = one(a1, 1, s0, c, pw1, (c + pw1 - 1) / pw1)) != hipSuccess) return e;
-            IkArgsT<T> a2 = at;  // phase 2: attempts 1.. of the listed targets, side by side
-            a2.att0 = 1;
+            IkArgsT<T> a2 = at;  // phase 2: attempts 1.. (0 resumed, after a hand-over) of the listed targets
+            a2.att0 = cut ? 0 : 1;
+            a2.cont = cut ? 1 : 0;
+            a2.p1_cut = cut;
+            a2.fail_aux = scr.fail_aux;
             a2.idx = scr.fail_list;
             a2.fail_ctl = scr.fail_ctl;
             a2.fail_mask = (uint32_t)(scr.cap - 1);
-            const int G2 = natt - 1 <= 1 ? 1 : natt - 1 <= 2 ? 2 : natt - 1 <= 4 ? 4 : 8;
+            const int na2 = natt - a2.att0;
+            const int G2 = na2 <= 1 ? 1 : na2 <= 2 ? 2 : na2 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
             if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
                 // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;

@@ -13,6 +13,33 @@ namespace {
 #ifndef KINHIP_IK_FAST_ATAN
 #define KINHIP_IK_FAST_ATAN 1  // fp32: polynomial atan2 for the rotation error's angle (rot_error)
 #endif
+// Diagnostic section stamps (tools only: KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=<k> in the A/B build): the
+// cycles of iteration section k (1 FK, 2 errors + checks, 3 Jacobian + J W J^T, 4 Cholesky + solves,
+// 5 dq + active set, 6 step, 7 loop top) summed over the lane's iterations replace err row 0 and the
+// lane's cycles from its first iteration to its write replace err row 1.  Never in a product build.
+#ifndef KINHIP_IK_SECT
+#define KINHIP_IK_SECT 0
+#endif
+#if KINHIP_IK_SECT
+__device__ __forceinline__ uint64_t ik_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define KIN_IK_STAMP(k)                                   \
+    do {                                                  \
+        const uint64_t t_ = ik_stamp();                   \
+        if ((k) == KINHIP_IK_SECT) sect_acc += t_ - sect_prev; \
+        sect_prev = t_;                                   \
+    } while (0)
+#else
+#define KIN_IK_STAMP(k) \
+    do {                \
+    } while (0)
+#endif
+
 #if KINHIP_IK_NARROW
 #define KIN_IK_LD ldn_soa
 #define KIN_IK_ST stn_soa
@@ -84,14 +111,15 @@ __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (
 #else
     const T th = atan2_t(s, c);
 #endif
-    if (s > T(1e-7)) {
-        T k;
-        if constexpr (sizeof(T) == 4) k = th * rcp_fast(s);
-        else k = th / s;
-        w[0] = v0 * k; w[1] = v1 * k; w[2] = v2 * k;
-    } else if (c > T(0)) {
-        w[0] = v0; w[1] = v1; w[2] = v2;
-    } else {
+    // common cases without a branch: k = th / s, or 1 for s <= 1e-7 (w = v exactly); only the
+    // rotation by ~pi (s tiny, c < 0) takes the branch
+    const bool tiny = !(s > T(1e-7));
+    T kth;
+    if constexpr (sizeof(T) == 4) kth = th * rcp_fast(s);
+    else kth = th / s;
+    kth = tiny ? T(1) : kth;
+    w[0] = v0 * kth; w[1] = v1 * kth; w[2] = v2 * kth;
+    if (tiny & !(c > T(0))) {
         int b = 0;
         if (E[4] > E[0]) b = 1;
         if (E[8] > E[4 * b]) b = 2;
@@ -136,6 +164,14 @@ struct IkArgsT {
     // residual [p* - p; rpy* - rpy] (angle differences wrapped to (-pi, pi]) with the rpy_jac=true
     // Jacobian rows, converged on |dp| < tol_pos and |d rpy| < tol_rot; 0: the axis-angle residual
     int32_t rpy_obj;
+    // Early hand-over (two-phase schedule): phase 1 stops attempt 0 of a target that is not solved
+    // after p1_cut iterations (0: runs the whole attempt) and lists it with its state -- the angles
+    // in q (and base in q's base columns), the active set in fail_aux at the same ring position;
+    // phase 2 (cont = 1, att0 = 0) resumes attempt 0 there on slot 0 beside attempts 1, 2, ...
+    // The resumed trajectory is the uninterrupted one bit for bit (nothing else carries over).
+    int32_t p1_cut;
+    int32_t cont;
+    int32_t* fail_aux;
 };
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
@@ -208,6 +244,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
     int64_t i = 0;
+    uint32_t rpos = 0;    // phase 2: ring position of this target (fail_aux)
     bool have = false;    // the first pass of the loop hands every group its first target
     const bool base = (P.flags & PF_BASE) != 0;
     const int L = a.attempt_len;
@@ -217,9 +254,13 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     T trpy[3] = {T(0), T(0), T(0)};  // rpy of the target (reference objective)
     uint32_t blk = 0;  // active set: joints held out of the solve (bit s = phase-A step s)
     int att = 0, it = 0, res_att = INT_MAX;
+    int att_end = INT_MAX;  // iteration at which this lane's attempt is over (the schedule's it % L == 0)
     bool done = true, final_lane = false;
     uint32_t off = 0;
     T ep = 0, er = 0;
+#if KINHIP_IK_SECT
+    uint64_t sect_acc = 0, sect_prev = 0, sect_t0 = 0;
+#endif
     auto start_target = [&]() {
         off = (uint32_t)i * (uint32_t)sizeof(T);
 #pragma unroll
@@ -243,9 +284,26 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         it = att > 0 ? att * L + 1 : 0;
         ep = er = T(0);
         blk = 0;
-        ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
+        att_end = L > 0 ? (att + 1) * L : INT_MAX;
+        if (a.phase1 && a.p1_cut) att_end = a.p1_cut;  // phase 1: attempt 0 only, handed over there
+        if (a.cont && att == 0) {  // resume attempt 0 where phase 1 handed it over
+            it = a.p1_cut;
+            blk = (uint32_t)a.fail_aux[rpos];
+#pragma unroll
+            for (int s = 0; s < MAXA; ++s) {
+                const int32_t c = S[s].qcol;
+                qs[s] = c >= 0 ? KIN_IK_LD(q, c, ldq, off) : T(0);
+            }
+            if (base)
+                for (int k = 0; k < 3; ++k) b[k] = KIN_IK_LD(q, P.base_col + k, ldq, off);
+        } else {
+            ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
+        }
     };
     T ro[MAXA][3], rz[MAXA][3];
+    // wave-uniform: lanes without a target that can get none (the wave's range is drained); while the
+    // lanes that are done are exactly these, the bookkeeping below has nothing to do and is skipped
+    uint64_t settled = 0;
     for (;;) {
         int gm = res_att;  // lowest converged attempt of this lane group's target so far
         if constexpr (G > 1) {
@@ -255,11 +313,23 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
         // a group whose lanes are all done writes its target and takes the next one
         const uint64_t dmask = __ballot(!have || done);
+        if (dmask != settled) {  // (wave-uniform)
         const bool gfin = have && (dmask & gmask) == gmask;
         if (gfin) {
             const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
-            if (a.phase1 && res_att == INT_MAX) {  // attempt 0 failed: phase 2 takes the target
-                a.fail_list[atomicAdd(&a.fail_ctl[0], 1u) & a.fail_mask] = (int32_t)i;
+            if (a.phase1 && res_att == INT_MAX) {  // attempt 0 failed or was handed over: phase 2 takes it
+                const uint32_t pos = atomicAdd(&a.fail_ctl[0], 1u) & a.fail_mask;
+                a.fail_list[pos] = (int32_t)i;
+                if (a.p1_cut) {  // hand-over state (see IkArgsT)
+                    a.fail_aux[pos] = (int32_t)blk;
+#pragma unroll
+                    for (int s2 = 0; s2 < MAXA; ++s2) {
+                        const int32_t c = S[s2].qcol;
+                        if (c >= 0) KIN_IK_ST(q, c, ldq, off, qs[s2]);
+                    }
+                    if (base)
+                        for (int k = 0; k < 3; ++k) KIN_IK_ST(q, P.base_col + k, ldq, off, b[k]);
+                }
             } else if (writer) {
 #pragma unroll
                 for (int s2 = 0; s2 < MAXA; ++s2) {
@@ -269,6 +339,10 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 if (base)
                     for (int k = 0; k < 3; ++k) KIN_IK_ST(q, P.base_col + k, ldq, off, b[k]);
                 if (iters) iters[i] = it;
+#if KINHIP_IK_SECT
+                ep = (T)(double)sect_acc;
+                er = (T)(double)(ik_stamp() - sect_t0);
+#endif
                 if (err) {
                     KIN_IK_ST(err, 0, lde, off, ep);
                     KIN_IK_ST(err, 1, lde, off, er);
@@ -281,18 +355,26 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             const uint64_t lead = 1ull << (grp * G);
             const int rank = __popcll(need & (lead - 1ull));
             if (!have && (need & lead) && next + rank < wend) {
-                i = a.idx ? (int64_t)a.idx[(fbeg + (uint32_t)(next + rank)) & a.fail_mask] : next + rank;
+                rpos = (fbeg + (uint32_t)(next + rank)) & a.fail_mask;
+                i = a.idx ? (int64_t)a.idx[rpos] : next + rank;
                 have = true;
                 start_target();  // the single (inlined) initialisation site
             }
             next += __popcll(need);
         }
         if (__ballot(have) == 0) break;  // wave-uniform exit: range drained, every target written
+        settled = next >= wend ? __ballot(!have) : 0ull;
+        }
         if (!have || done) continue;
+#if KINHIP_IK_SECT
+        if (sect_t0 == 0) sect_t0 = sect_prev = ik_stamp();
+#endif
+        KIN_IK_STAMP(7);
         Fr<T> root, L_;
         if (base) base_frame(root, b[0], b[1], b[2]);
         else set_identity(root);
         chain_records<T, MAXA>(P, S, root, qs, L_, ro, rz);
+        KIN_IK_STAMP(1);
         const Fr<T>& Lf = L_;
         T e[6];
         e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
@@ -312,30 +394,34 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
             er = sqrt_fast(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
-        if (ep < a.tol_pos && er < a.tol_rot) {
-            res_att = att;
-            done = true;
-            continue;
-        }
-        if (it >= a.max_iters) {  // only the last attempt gets here
-            final_lane = true;
-            it = a.max_iters + 1;  // not converged (kinhip.h: iters > max_iters)
-            done = true;
-            continue;
-        }
-        if (L > 0 && it > 0 && it % L == 0) {  // attempt over: this lane's next one, if any
-            att += G;
-            if (att >= a.n_attempts) {
+        // the rare ends of an iteration behind one branch (bitwise, so the common path carries no
+        // exec-mask bookkeeping): converged, out of iterations (only the last attempt gets there),
+        // attempt over (phase 1 with a hand-over: the target goes to phase 2)
+        const bool conv = (ep < a.tol_pos) & (er < a.tol_rot);
+        if (conv | (it >= a.max_iters) | (it == att_end)) {
+            if (conv) {
+                res_att = att;
                 done = true;
-            } else {
-                it = att * L + 1;
-                ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
-                b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
-                blk = 0;
+            } else if (it >= a.max_iters) {
+                final_lane = true;
+                it = a.max_iters + 1;  // not converged (kinhip.h: iters > max_iters)
+                done = true;
+            } else {  // attempt over: this lane's next one, if any
+                att += G;
+                if (att >= a.n_attempts) {
+                    done = true;
+                } else {
+                    it = att * L + 1;
+                    att_end = (att + 1) * L;
+                    ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + i, att, qs);
+                    b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
+                    blk = 0;
+                }
             }
             continue;
         }
 
+        KIN_IK_STAMP(2);
         T Jb[3][ROWS];
         if (base) {
 #pragma unroll
@@ -351,6 +437,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         // linear Jacobian rows z x (p - o) once per iteration (the solve and dq reuse them)
 #pragma unroll
         for (int s = 0; s < MAXA; ++s) {
+            if (S[s].jkind == MOT_PRISM) continue;  // [z; 0] (jcol_pre): no lever arm
             const T dx = Lf.t[0] - ro[s][0], dy = Lf.t[1] - ro[s][1], dz = Lf.t[2] - ro[s][2];
             ro[s][0] = fma(rz[s][1], dz, -(rz[s][2] * dy));
             ro[s][1] = fma(rz[s][2], dx, -(rz[s][0] * dz));
@@ -391,10 +478,17 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r) J[r] *= ws;
                 }
+                if (ROWS == 6 && S[s].jkind == MOT_PRISM) {  // angular rows zero: the linear block only
 #pragma unroll
-                for (int r = 0; r < ROWS; ++r)
+                    for (int r = 0; r < 3; ++r)
 #pragma unroll
-                    for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+                        for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                        for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+                }
             }
             if (base) {
 #pragma unroll
@@ -404,6 +498,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
                         for (int c = 0; c <= r; ++c) A[r][c] = fma(Jb[k][r], Jb[k][c], A[r][c]);
             }
+            KIN_IK_STAMP(3);
             // Cholesky A = L L^T (in place, lower), then y = A^-1 e.  fp32 keeps the
             // reciprocal square root of each pivot (hardware v_rsq_f32) and multiplies:
             // the 6 square roots and 27 divisions of the IEEE form are ~10 instructions
@@ -448,17 +543,22 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 if constexpr (fast) y[r] = sm * ip[r];
                 else y[r] = sm / A[r][r];
             }
+            KIN_IK_STAMP(4);
             uint32_t nb = 0;
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
                 jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
                 T v = T(0);
+                const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;  // (zero angular rows)
 #pragma unroll
-                for (int r = 0; r < ROWS; ++r) v = fma(J[r], y[r], v);
+                for (int r = 0; r < ROWS; ++r)
+                    if (r < nr) v = fma(J[r], y[r], v);
                 const bool held = (blk >> s) & 1u;
                 dq[s] = held ? T(0) : v;
-                if ((qs[s] <= S[s].lo && v < T(0)) || (qs[s] >= S[s].hi && v > T(0))) nb |= 1u << s;
+                // pushed further out of a limit it sits on (selects, no short-circuit branches)
+                const T out_lo = qs[s] <= S[s].lo ? -v : T(0), out_hi = qs[s] >= S[s].hi ? v : T(0);
+                nb |= (out_lo > T(0)) | (out_hi > T(0)) ? 1u << s : 0u;
                 mx = fmax(mx, fabs(dq[s]));
             }
             blk = nb;
@@ -473,12 +573,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 }
             }
         }
+        KIN_IK_STAMP(5);
         const T sc = mx > a.max_step ? a.max_step / mx : T(1);
 #pragma unroll
         for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(qs[s] + sc * dq[s], S[s].lo), S[s].hi);
         if (base)
             for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
         ++it;
+        KIN_IK_STAMP(6);
     }
 }
 

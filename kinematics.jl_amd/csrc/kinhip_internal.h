@@ -77,6 +77,7 @@ struct IkArgs {
 // not solve and its length, for batches of up to `cap` targets (null: single phase only)
 struct IkScratch {
     int32_t* fail_list = nullptr;
+    int32_t* fail_aux = nullptr;   // per ring entry: the handed-over active set (IkArgsT::p1_cut)
     uint32_t* fail_ctl = nullptr;  // 3 control words of the ring (IkArgsT), zero at allocation
     int64_t cap = 0;               // ring entries, a power of two
 };

@@ -95,13 +95,20 @@ def test_oracle_collision_fd(with_base):
 
 
 # ------------------------------------------------------------------ GPU ------
-def _assert_mismatches_at_kinks(om, box, Q, ids, sph, rad, g_gpu, g_ref, gtol, h=1e-7):
+def _assert_mismatches_at_kinks(om, box, Q, ids, sph, rad, g_gpu, g_ref, gtol, h=1e-7, boxes=None, dtie=0.0):
     """Every gradient entry where the GPU's analytic gradient and the reference's forward-difference
     gradient (src/sdf.jl:34-41, eps 1e-7) differ by more than gtol must sit where the distance is not
     differentiable at the reference's own step: its one-sided differences in q (step h) to the right
     and to the left disagree by more than gtol (a box kink -- union argmin switch, inside medial plane,
     the surface -- or the edge region within ~1e-3 of a box where eps-sized differences lose the
-    derivative).  Returns the number of such entries."""
+    derivative), or the reference's forward difference is the inaccurate one: near a box edge the
+    distance's curvature ~1/r makes the eps = 1e-7 forward difference off by ~eps/(2r) while the
+    one-sided slopes differ by less than gtol; such an entry must match the central difference of the
+    exact distance (step h) to within gtol/4 and sit farther from it than the GPU's value does.
+    With boxes = (poses, widths) of the union and dtie > 0 (fp32: the distance bound), an entry may also
+    be an argmin near-tie: another box's distance within dtie of the union's minimum (the two are
+    indistinguishable at the kernel's precision) whose own gradient the GPU's value matches to gtol.
+    Returns the number of such entries."""
     gtol = np.broadcast_to(np.asarray(gtol, np.float64), g_gpu.shape)  # scalar or per entry
     bad = np.argwhere(np.abs(g_gpu - g_ref) > gtol)  # (sphere k, dof i, config n)
     if bad.size == 0:
@@ -119,7 +126,20 @@ def _assert_mismatches_at_kinks(om, box, Q, ids, sph, rad, g_gpu, g_ref, gtol, h
     for j, (k, i, n) in enumerate(bad):
         right = (d_pm[k, 2 * j] - d0[k, j]) / h
         left = (d0[k, j] - d_pm[k, 2 * j + 1]) / h
-        assert abs(right - left) > gtol[k, i, n], (k, i, n, right, left, g_gpu[k, i, n], g_ref[k, i, n])
+        if abs(right - left) > gtol[k, i, n]:
+            continue  # a kink: the two one-sided derivatives differ
+        central = 0.5 * (right + left)
+        if (abs(g_gpu[k, i, n] - central) <= 0.25 * gtol[k, i, n]
+                and abs(g_ref[k, i, n] - central) > abs(g_gpu[k, i, n] - central)):
+            continue  # the reference's forward difference is the inaccurate one
+        assert boxes is not None and dtie > 0, (k, i, n, right, left, g_gpu[k, i, n], g_ref[k, i, n])
+        tie = False
+        for pose, w in zip(*boxes):  # argmin near-tie: another box at the minimum to within dtie
+            db, gb = O.coll_batch(om, O.OracleUnionSDF([pose], [w]), q[:, n:n + 1], ids, sph, rad)
+            if db[k, 0] - d0[k, j] <= dtie and abs(gb[k, i, 0] - g_gpu[k, i, n]) <= gtol[k, i, n]:
+                tie = True
+                break
+        assert tie, (k, i, n, right, left, g_gpu[k, i, n], g_ref[k, i, n])
     return len(bad)
 
 
@@ -244,10 +264,7 @@ def test_gpu_collision_lds_box_limit(n_boxes):
     spe = sscc.plan(arm, dtype=torch.float32).specialize()
     D0, G0, M0 = gen.run(sdf, Q, grads=True, min_dist=True)
     D1, G1, M1 = spe.run(sdf, Q, grads=True, min_dist=True)
-    # distances and minima bit-equal; gradients to a few ulp (the two compilations contract the
-    # argmin box's gradient product-sums differently; measured <= 3e-7, tools/coll_spec_diff.py)
-    assert torch.equal(D0, D1) and torch.equal(M0, M1)
-    torch.testing.assert_close(G0, G1, atol=1e-6, rtol=0)
+    assert torch.equal(D0, D1) and torch.equal(G0, G1) and torch.equal(M0, M1)
     tree, om, sph, rad = _fetch_with_spheres(False)
     box = O.OracleUnionSDF(poses, widths)
     ids = [tree.joint_id(n) for n in ARM]
@@ -354,22 +371,18 @@ def test_gpu_collision_specialized_equals_generic(dtype, with_base):
     gen = sscc.plan(arm, dtype=dtype)
     spe = sscc.plan(arm, dtype=dtype).specialize()
     assert spe.specialized == kinhip.KIN_SPEC_COLL
-    gtol = 1e-6 if dtype == torch.float32 else 1e-15  # gradients: a few ulp (see test_gpu_collision_lds_box_limit)
     for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True),
                dict(dists=True, grads=True, truncation=0.1)):
-        for k, (x, y) in enumerate(zip(gen.run(sdf, Q, **kw), spe.run(sdf, Q, **kw))):
-            if k == 1 and x is not None:
-                torch.testing.assert_close(x, y, atol=gtol, rtol=0)
-            else:
-                assert (x is None and y is None) or torch.equal(x, y), kw
+        for x, y in zip(gen.run(sdf, Q, **kw), spe.run(sdf, Q, **kw)):
+            assert (x is None and y is None) or torch.equal(x, y), kw
     if not with_base:  # two chains (arm + head)
         sscc.add_coll_sphere(m.find_link("head_pan_link"), (0.05, 0.0, 0.1), 0.12)
         joints = arm + [m.find_joint("head_pan_joint"), m.find_joint("head_tilt_joint")]
         Q2 = (torch.rand((10, N), generator=g, dtype=torch.float64) * 2 - 1).to(dtype).to(dev)
         a = sscc.plan(joints, dtype=dtype).run(sdf, Q2, grads=True, min_dist=True)
         b = sscc.plan(joints, dtype=dtype).specialize().run(sdf, Q2, grads=True, min_dist=True)
-        assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
-        torch.testing.assert_close(a[1], b[1], atol=1e-6 if dtype == torch.float32 else 1e-15, rtol=0)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
 
 
 @pytest.mark.gpu

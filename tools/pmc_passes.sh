@@ -1,7 +1,7 @@
 #!/bin/bash
-# rocprofv3 passes for the round-2 profiles: per workload a kernel trace + stats, then separate
+# rocprofv3 passes for the round profiles: per workload a kernel trace + stats, then separate
 # --pmc passes (never combined with trace domains; each pass within the per-block counter limits).
-#   bash tools/pmc_r02.sh <tag>:<prof_kernel workload>[:extra args] ...
+#   bash tools/pmc_passes.sh <tag>:<prof_kernel workload>[:extra args] ...
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof
