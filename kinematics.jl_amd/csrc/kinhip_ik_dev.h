@@ -10,6 +10,9 @@ namespace {
 #ifndef KINHIP_IK_NARROW
 #define KINHIP_IK_NARROW 0  // 1: narrow SoA addressing (ldn_soa) in k_ik_dls, see kinhip_device.h
 #endif
+#ifndef KINHIP_IK_PK
+#define KINHIP_IK_PK 1  // fp32: packed FMAs for J W J^T (ik_body)
+#endif
 #ifndef KINHIP_IK_FAST_ATAN
 #define KINHIP_IK_FAST_ATAN 1  // fp32: polynomial atan2 for the rotation error's angle (rot_error)
 #endif
@@ -469,6 +472,18 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int r = 0; r < ROWS; ++r)
 #pragma unroll
                 for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? a.lam2 : T(0);
+            // fp32: entries (r, 2k) and (r, 2k + 1) in one packed FMA (v_pk_fma_f32, J[r] broadcast):
+            // 12 instead of 21 per joint, each element the same fma (identical results).  One wave per
+            // SIMD issues a packed FMA in ~1.5x the time of a scalar one (tools/pk_probe.hip).
+            constexpr bool pk = KINHIP_IK_PK && sizeof(T) == 4 && ROWS == 6;
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            f2 A2[pk ? ROWS : 1][pk ? ROWS / 2 : 1];
+            if constexpr (pk) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                    for (int k = 0; k < ROWS / 2; ++k) A2[r][k] = f2{(float)A[r][2 * k], (float)A[r][2 * k + 1]};
+            }
 #pragma unroll
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
@@ -478,17 +493,29 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r) J[r] *= ws;
                 }
-                if (ROWS == 6 && S[s].jkind == MOT_PRISM) {  // angular rows zero: the linear block only
+                const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;  // prismatic: linear block only
+                if constexpr (pk) {
+                    const f2 Jp[3] = {f2{(float)J[0], (float)J[1]}, f2{(float)J[2], (float)J[3]},
+                                      f2{(float)J[4], (float)J[5]}};
 #pragma unroll
-                    for (int r = 0; r < 3; ++r)
+                    for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-                        for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+                        for (int k = 0; k <= r / 2; ++k)
+                            if (r < nr && 2 * k < nr)
+                                A2[r][k] = __builtin_elementwise_fma(f2{(float)J[r], (float)J[r]}, Jp[k], A2[r][k]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-                        for (int c = 0; c <= r; ++c) A[r][c] = fma(J[r], J[c], A[r][c]);
+                        for (int c = 0; c <= r; ++c)
+                            if (r < nr) A[r][c] = fma(J[r], J[c], A[r][c]);
                 }
+            }
+            if constexpr (pk) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+                    for (int c = 0; c <= r; ++c) A[r][c] = (T)((c & 1) ? A2[r][c / 2].y : A2[r][c / 2].x);
             }
             if (base) {
 #pragma unroll

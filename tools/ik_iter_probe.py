@@ -14,9 +14,10 @@ m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
 arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
 gl = m.find_link("gripper_link")
 dt = torch.float64 if os.environ.get("AB_F64") else torch.float32
+NS = [int(x) for x in os.environ.get("IK_NS", "65536,131072,262144").split(",")]
 plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt).specialize()
 rot = int(os.environ.get("AB_ROT", "1"))
-for n in (65536, 131072, 262144):
+for n in NS:
     Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=4242, dtype=dt,
                                 device=dev)
     tgt = plan.run(Qt)[0][0].contiguous()
