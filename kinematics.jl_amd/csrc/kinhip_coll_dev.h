@@ -34,6 +34,21 @@ __device__ __forceinline__ T box_key(T qx, T qy, T qz) {
 __device__ __forceinline__ float signed_sqrt(float k) { return copysignf(__builtin_amdgcn_sqrtf(fabsf(k)), k); }
 __device__ __forceinline__ double signed_sqrt(double k) { return copysign(sqrt(fabs(k)), k); }
 
+// KINHIP_COLL_SOFF=1 (the specialised kernels, kinhip_jit.cpp): rows addressed through soffset
+// (ldo_soa / sto_soa, kinhip_device.h); the launcher runs them only within that addressing's bound
+#ifndef KINHIP_COLL_SOFF
+#define KINHIP_COLL_SOFF 0
+#endif
+#if KINHIP_COLL_SOFF
+#define KIN_CO_LD ldo_soa
+#define KIN_CO_ST sto_soa
+#define KIN_CO_ST2 sto_soa2
+#else
+#define KIN_CO_LD ld_soa
+#define KIN_CO_ST st_soa
+#define KIN_CO_ST2 st_soa2
+#endif
+
 #ifndef KINHIP_AABB_UNROLL
 #define KINHIP_AABB_UNROLL 2
 #endif
@@ -59,9 +74,7 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
         bk[i] = 0;
     }
     // uniform loops, box data through the scalar cache; argmin keeps the first minimum (Julia's argmin)
-#pragma clang loop vectorize(disable) unroll_count(KINHIP_AABB_UNROLL)
-    for (int k = 0; k < na; ++k) {  // axis-aligned boxes: no rotation
-        const KAabb<T>& b = aabb[k];
+    auto aabb_box = [&](const KAabb<T>& b, int k) {  // axis-aligned boxes: no rotation
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             const T key = box_key(fabs(px[i] - b.c[0]) - b.half[0], fabs(py[i] - b.c[1]) - b.half[1],
@@ -75,7 +88,19 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
                 best[i] = fmin(best[i], key);
             }
         }
+    };
+    // KINHIP_AABB_UNROLL boxes per trip through one pointer that moves by whole trips, so every scalar
+    // load sits at a non-negative immediate offset from it (an unroll pragma let the loop-strength
+    // reduction base the pointer on the last box and rebuild each earlier address with 64-bit SALU adds)
+    const KAabb<T>* __restrict__ ab = aabb;
+    int k = 0;
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (; k + KINHIP_AABB_UNROLL <= na; k += KINHIP_AABB_UNROLL, ab += KINHIP_AABB_UNROLL) {
+#pragma unroll
+        for (int u = 0; u < KINHIP_AABB_UNROLL; ++u) aabb_box(ab[u], k + u);
     }
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (; k < na; ++k, ++ab) aabb_box(ab[0], k);
 #pragma clang loop vectorize(disable)
     for (int k = na; k < nb; ++k) {
         const KBox<T>& b = boxes[k];
@@ -125,7 +150,10 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
             const T mx = fmax(q[0], fmax(q[1], q[2]));
             if (mx > T(0)) {  // outside: d = |max(q, 0)|
                 const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
-                const T rn = T(1) / sqrt_t(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+                const T oo = o[0] * o[0] + o[1] * o[1] + o[2] * o[2];
+                T rn;  // fp32: hardware v_rsq_f32 (1 ulp) instead of the ~10-instruction IEEE division
+                if constexpr (sizeof(T) == 4) rn = rsqrt_fast(oo);
+                else rn = T(1) / sqrt_t(oo);
 #pragma unroll
                 for (int j = 0; j < 3; ++j) gl[j] = (l[j] < T(0) ? -o[j] : o[j]) * rn;
             } else {  // inside: d = max(q)
@@ -321,7 +349,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         }
         d -= offs;  // IneqConst: dist - margin (src/planning.jl:66)
         dmin = fmin(dmin, d);
-        if (dists) st_soa(dists, sp.out, ldd, off, d);
+        if (dists) KIN_CO_ST(dists, sp.out, ldd, off, d);
         if constexpr (GRAD && KINHIP_COLL_STPAIR && KINHIP_JIT && sizeof(T) == 4) {
             constexpr int NC = 16;
             if (ndof <= NC && pair_ok) {  // uniform
@@ -360,10 +388,10 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                     if (c + 1 < ndof) {
                         const T send = par ? cv[c] : cv[c + 1];
                         const T recv = __shfl_xor(send, 1);
-                        st_soa2(grads, r0 + c + par, ldg, off - (uint32_t)par * 4u, par ? recv : cv[c],
+                        KIN_CO_ST2(grads, r0 + c + par, ldg, off - (uint32_t)par * 4u, par ? recv : cv[c],
                                 par ? cv[c + 1] : recv);
                     } else if (c < ndof) {
-                        st_soa(grads, r0 + c, ldg, off, cv[c]);
+                        KIN_CO_ST(grads, r0 + c, ldg, off, cv[c]);
                     }
                 }
                 return;
@@ -375,7 +403,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
             while (zm) {
                 const int c = __builtin_ctzll(zm);
                 zm &= zm - 1;
-                st_soa(grads, r0 + c, ldg, off, T(0));
+                KIN_CO_ST(grads, r0 + c, ldg, off, T(0));
             }
             // column j = g . (z_j x (p - o_j)) = z_j . (p x g) - g . m_j with m_j = z_j x o_j
             // precomputed per configuration (k_coll), so a column costs 6 FMA instead of 12
@@ -395,15 +423,15 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                     while (m) {
                         const int c = __builtin_ctzll(m);
                         m &= m - 1;
-                        st_soa(grads, r0 + c, ldg, off, v);
+                        KIN_CO_ST(grads, r0 + c, ldg, off, v);
                     }
                 }
             }
             if (P.flags & PF_BASE) {  // base columns [1 0 -y; 0 1 x; 0 0 0] (src/algorithm.jl:98-103)
                 const int64_t b0 = r0 + P.n_jac;
-                st_soa(grads, b0 + 0, ldg, off, cut ? T(0) : g[0]);
-                st_soa(grads, b0 + 1, ldg, off, cut ? T(0) : g[1]);
-                st_soa(grads, b0 + 2, ldg, off, cut ? T(0) : fma(-g[0], py - by, g[1] * (px - bx)));
+                KIN_CO_ST(grads, b0 + 0, ldg, off, cut ? T(0) : g[0]);
+                KIN_CO_ST(grads, b0 + 1, ldg, off, cut ? T(0) : g[1]);
+                KIN_CO_ST(grads, b0 + 2, ldg, off, cut ? T(0) : fma(-g[0], py - by, g[1] * (px - bx)));
             }
         }
     };
@@ -461,15 +489,15 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     const bool base = (P.flags & PF_BASE) != 0;
     T bx = T(0), by = T(0), bth = T(0);
     if (base) {
-        bx = ld_soa(q, P.base_col, ldq, off);
-        by = ld_soa(q, P.base_col + 1, ldq, off);
-        bth = ld_soa(q, P.base_col + 2, ldq, off);
+        bx = KIN_CO_LD(q, P.base_col, ldq, off);
+        by = KIN_CO_LD(q, P.base_col + 1, ldq, off);
+        bth = KIN_CO_LD(q, P.base_col + 2, ldq, off);
     }
     T qa[MAXA];
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;
-        qa[s] = c >= 0 ? ld_soa(q, c, ldq, off) : T(0);
+        qa[s] = c >= 0 ? KIN_CO_LD(q, c, ldq, off) : T(0);
     }
     Fr<T> f;
     if (base) base_frame(f, bx, by, bth);
@@ -505,8 +533,8 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
                                            smem, use_lds, &sc);
     }
     if (min_dist) {
-        if (a.accumulate) dmin = fmin(dmin, ld_soa(min_dist, 0, 0, off));
-        st_soa(min_dist, 0, 0, off, dmin);
+        if (a.accumulate) dmin = fmin(dmin, KIN_CO_LD(min_dist, 0, 0, off));
+        KIN_CO_ST(min_dist, 0, 0, off, dmin);
     }
 }
 

@@ -201,6 +201,32 @@ __device__ __forceinline__ void stn_soa(double* __restrict__ base, int64_t row, 
                                           (int)(off + (uint32_t)(row * ld * 8)), 0, KINHIP_STORE_AUX);
 }
 
+// "Row in soffset" SoA addressing: one buffer descriptor per array, the row's byte offset in the
+// instruction's scalar offset (soffset) and the lane offset in the VGPR.  A row costs one scalar
+// multiply-add for its offset instead of the 64-bit add plus descriptor rebuild (3 SALU) of
+// ld_soa / st_soa -- the collision gradient kernel stores 126 rows per sample.  Valid while
+// (rows * ld + lane span) * sizeof(T) < 2^31 (the launcher checks; kinhip_jit.cpp builds the
+// specialised collision kernels with it, KINHIP_COLL_SOFF).
+__device__ __forceinline__ float ldo_soa(const float* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base), (int)off, (int)(row * ld * 4), 0));
+}
+__device__ __forceinline__ double ldo_soa(const double* __restrict__ base, int64_t row, int64_t ld, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(row_rsrc(base), (int)off, (int)(row * ld * 8), 0));
+}
+__device__ __forceinline__ void sto_soa(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base), (int)off, (int)(row * ld * 4),
+                                          KINHIP_STORE_AUX);
+}
+__device__ __forceinline__ void sto_soa2(float* __restrict__ base, int64_t row, int64_t ld, uint32_t off, float lo,
+                                         float hi) {
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(lo), __float_as_uint(hi)}, row_rsrc(base), (int)off,
+                                          (int)(row * ld * 4), KINHIP_STORE_AUX);
+}
+__device__ __forceinline__ void sto_soa(double* __restrict__ base, int64_t row, int64_t ld, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), row_rsrc(base), (int)off, (int)(row * ld * 8),
+                                          KINHIP_STORE_AUX);
+}
+
 template <typename T>
 __device__ __forceinline__ void set_identity(Fr<T>& f) {
 #pragma unroll

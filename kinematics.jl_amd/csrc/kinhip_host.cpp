@@ -1508,19 +1508,27 @@ namespace {
 int coll_launch(const kin_plan* p, const kin_sdf* sdf, CollArgs a, const void* q, int64_t ldq, int64_t n, void* dists,
                 int64_t ldd, void* grads, int64_t ldg, void* min_dist, const TileArgs& ta, void* stream) {
     const size_t np = p->parts.empty() ? 1 : p->parts.size();
+    // the specialised kernels address rows through the scalar offset (KINHIP_COLL_SOFF): every row
+    // offset plus the lane span must stay below 2^31 bytes, else the generic kernels run
+    const int64_t esz = p->dtype == KIN_F32 ? 4 : 8;
+    const bool tiled = ta.tile < n;
+    const int64_t span = tiled ? ta.tile : std::min<int64_t>(n, kChunk);
+    const auto fits = [&](int64_t rows, int64_t ld) { return ((rows + 1) * (tiled ? ta.tile : ld) + span) * esz < (int64_t(1) << 31); };
+    const bool soff = fits(p->nqcols, ldq) && (!dists || fits(p->n_sph, ldd)) &&
+                      (!grads || fits((int64_t)p->n_sph * p->nqcols, ldg));
     for (size_t k = 0; k < np; ++k) {
         const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
         a.accumulate = k > 0;
+        const JitFns* jf = soff ? jit_fns(s->jit) : nullptr;
         hipError_t e;
         if (s->dtype == KIN_F32)
             e = launch_coll<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
                                    (const KBox<float>*)sdf->d_f32, s->geom, a, (const float*)q, ldq, n, (float*)dists,
-                                   ldd, (float*)grads, ldg, (float*)min_dist, ta, jit_fns(s->jit),
-                                   (hipStream_t)stream);
+                                   ldd, (float*)grads, ldg, (float*)min_dist, ta, jf, (hipStream_t)stream);
         else
             e = launch_coll<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
                                     (const KBox<double>*)sdf->d_f64, s->geom, a, (const double*)q, ldq, n,
-                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, ta, jit_fns(s->jit),
+                                    (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, ta, jf,
                                     (hipStream_t)stream);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll launch: ") + hipGetErrorString(e));
     }
