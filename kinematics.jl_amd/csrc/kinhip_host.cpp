@@ -1693,7 +1693,12 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     // that schedule touches it, so every other call stays allocation-free (capture-safe)
     IkScratch scr;
     if (ik_wants_two_phase(a, n, kin_plan::kIkScratchCap)) {
-        const size_t set_bytes = 2 * sizeof(int32_t) * kin_plan::kIkScratchCap + 256;  // ring + aux ring
+        // kIkSubRings rings of 2 * cap / kIkSubRings entries (a phase-1 launch spreads its hand-overs over
+        // the rings by wave; twice the even share covers the uneven last waves), list + aux, and the
+        // rings' control words (one 128-byte line each)
+        const int64_t ring_cap = 2 * kin_plan::kIkScratchCap / kIkSubRings;
+        const size_t ctl_bytes = sizeof(uint32_t) * kIkCtlStride * kIkSubRings;
+        const size_t set_bytes = ctl_bytes + 2 * sizeof(int32_t) * (size_t)(ring_cap * kIkSubRings);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
         const bool capturing = cs == hipStreamCaptureStatusActive;
@@ -1722,9 +1727,10 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         if (set >= 0) {  // (no set left for a captured call: one phase)
             unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * set;
             scr.fail_ctl = (uint32_t*)base;
-            scr.fail_list = (int32_t*)(base + 256);
-            scr.fail_aux = scr.fail_list + kin_plan::kIkScratchCap;
+            scr.fail_list = (int32_t*)(base + ctl_bytes);
+            scr.fail_aux = scr.fail_list + ring_cap * kIkSubRings;
             scr.cap = kin_plan::kIkScratchCap;
+            scr.ring_cap = ring_cap;
         }
     }
     hipError_t e;

@@ -184,15 +184,18 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a1.phase1 = 1;
             a1.fail_list = scr.fail_list;
             a1.fail_ctl = scr.fail_ctl;
-            a1.fail_mask = (uint32_t)(scr.cap - 1);
+            a1.fail_mask = (uint32_t)(scr.ring_cap - 1);
             a1.fail_aux = scr.fail_aux;
             // early hand-over (IkArgsT::p1_cut): attempt 0 stops after `cut` iterations in phase 1 and
             // phase 2 resumes it on slot 0 beside the other attempts.  Phase 1 then lasts `cut`
             // iterations instead of L and phase 2 (16 targets per wave at G = 4) absorbs the handed-over
             // ones at no extra latency while it stays within ~2 waves per SIMD (one wave alone issues
-            // every other VALU slot).  Not for in-place calls of based plans (the hand-over would
-            // overwrite the start pose that attempts 1, 2, ... begin from).
-            const int cut = ik_p1_cut(L, P.flags & PF_BASE ? (q0 != nullptr) : true);
+            // every other VALU slot).  Only while phase 1 is one round of resident waves: a larger
+            // batch is throughput-bound, and the hand-over would add the speculative attempts 1, 2, ...
+            // of every handed-over target that attempt 0 still solves (1M targets: 0.55 -> 0.59 ms).
+            // Not for in-place calls of based plans (the hand-over would overwrite the start pose that
+            // attempts 1, 2, ... begin from).
+            const int cut = (c + 63) / 64 <= resident_waves ? ik_p1_cut(L, P.flags & PF_BASE ? (q0 != nullptr) : true) : 0;
             a1.p1_cut = cut;
             // phase 1 shares out targets like the one-phase schedule (one per lane while the batch
             // fills the chip in at most two rounds of waves, else wave-local queues) -- but a queue
@@ -218,14 +221,14 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a2.fail_aux = scr.fail_aux;
             a2.idx = scr.fail_list;
             a2.fail_ctl = scr.fail_ctl;
-            a2.fail_mask = (uint32_t)(scr.cap - 1);
+            a2.fail_mask = (uint32_t)(scr.ring_cap - 1);
             const int na2 = natt - a2.att0;
             const int G2 = na2 <= 1 ? 1 : na2 <= 2 ? 2 : na2 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
             if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
                 // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;
                 // the targets phase 1 did not solve keep undefined outputs (kin_ik_dls_batch says so)
-                (void)hipMemsetAsync(scr.fail_ctl, 0, 3 * sizeof(uint32_t), st);
+                (void)hipMemsetAsync(scr.fail_ctl, 0, sizeof(uint32_t) * kIkCtlStride * kIkSubRings, st);
                 g_ik_partial = true;
                 return e;
             }

@@ -148,12 +148,14 @@ struct IkArgsT {
     // (one lane each) and appends the targets it does not solve to fail_list instead of writing
     // them; phase 2 runs attempts att0 = 1, 2, ... of the listed targets only (idx = fail_list).
     // Otherwise att0 = 0, phase1 = 0, idx = null.
-    // fail_list is a ring of fail_mask + 1 entries with three control words that are never reset
-    // between calls (so no memset launch precedes phase 1, and a captured graph replays as is):
-    // fail_ctl[0] = ring head (phase 1 appends at atomicAdd(head) & mask), fail_ctl[1] = this
-    // call's first entry (phase 1 copies it from fail_ctl[2]), fail_ctl[2] = the next call's
-    // first entry (phase 2 sets it to the head, after every phase-1 append).  Phase 2's targets
-    // are the entries [fail_ctl[1], fail_ctl[0]).
+    // fail_list holds kIkSubRings rings of fail_mask + 1 entries (phase-1 wave w appends to ring
+    // w % kIkSubRings, so the returning atomics of a launch spread over as many L2 lines instead of
+    // queueing on one: ~6 us for 1,024 waves on one head).  Each ring has three control words on a
+    // line of its own (fail_ctl + r * kIkCtlStride) that are never reset between calls (so no memset
+    // launch precedes phase 1, and a captured graph replays as is): [0] = ring head (phase 1 appends
+    // at atomicAdd(head) & mask), [1] = this call's first entry (phase 1 copies it from [2]), [2] =
+    // the next call's first entry (phase 2 sets it to the head, after every phase-1 append).  Phase
+    // 2's targets are the rings' entries [[1], [0]) in ring order (a prefix sum over the rings).
     int32_t att0;
     int32_t phase1;
     const int32_t* idx;
@@ -236,14 +238,30 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     const int lane = (int)(threadIdx.x & 63u);
     const int slot = lane % G, grp = lane / G;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    // two-phase control words (see IkArgsT): one lane of the grid moves the ring's start marks
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (a.phase1) a.fail_ctl[1] = a.fail_ctl[2];
-        else if (a.idx) a.fail_ctl[2] = a.fail_ctl[0];
+    // two-phase control words (see IkArgsT): one lane per ring of the grid's first wave moves its start marks
+    if (blockIdx.x == 0 && threadIdx.x < (unsigned)kIkSubRings && (a.phase1 || a.idx)) {
+        uint32_t* c = a.fail_ctl + threadIdx.x * kIkCtlStride;
+        if (a.phase1) c[1] = c[2];
+        else c[2] = c[0];
     }
-    const uint32_t fbeg = a.idx ? a.fail_ctl[1] : 0u;
+    // phase 2: lane r of every wave holds ring r's first entry and the number of listed targets
+    // before ring r (exclusive prefix over the rings); the wave's share is entries of that order
+    uint32_t ring_beg = 0, ring_excl = 0;
+    int64_t nt = n;
+    if (a.idx) {  // (uniform)
+        const uint32_t* c = a.fail_ctl + lane * kIkCtlStride;
+        ring_beg = c[1];
+        const uint32_t cnt = c[0] - ring_beg;
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int d = 1; d < kIkSubRings; d <<= 1) {
+            const uint32_t t = __shfl_up(inc, d);
+            if (lane >= d) inc += t;
+        }
+        ring_excl = inc - cnt;
+        nt = (int64_t)__shfl(inc, kIkSubRings - 1);  // phase 2: the listed targets only
+    }
     const T* __restrict__ qin = a.q0 ? a.q0 : q;  // uniform: where the starting angles are read
-    const int64_t nt = a.idx ? (int64_t)(uint32_t)(a.fail_ctl[0] - fbeg) : n;  // phase 2: the listed targets only
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
     int64_t i = 0;
@@ -263,6 +281,9 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     T ep = 0, er = 0;
 #if KINHIP_IK_SECT
     uint64_t sect_acc = 0, sect_prev = 0, sect_t0 = 0;
+    // KINHIP_IK_SECT=9: the lane's entry and write times (s_memrealtime, 100 MHz, low 32 bits as raw
+    // bits in err rows 0 / 1) to place each launch's waves on one clock
+    const uint32_t rt_entry = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
     auto start_target = [&]() {
         off = (uint32_t)i * (uint32_t)sizeof(T);
@@ -304,9 +325,6 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
     };
     T ro[MAXA][3], rz[MAXA][3];
-    // wave-uniform: lanes without a target that can get none (the wave's range is drained); while the
-    // lanes that are done are exactly these, the bookkeeping below has nothing to do and is skipped
-    uint64_t settled = 0;
     for (;;) {
         int gm = res_att;  // lowest converged attempt of this lane group's target so far
         if constexpr (G > 1) {
@@ -315,13 +333,33 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             if (have && !done && gm < att) done = true;
         }
         // a group whose lanes are all done writes its target and takes the next one
+        // While the wave's range still has targets, a finished group writes at once and takes the next;
+        // once every target is handed out (always, for a wave of at most 64 / G targets) the finished
+        // groups keep their results in registers and the whole wave writes when its last lane is
+        // done: no stores and no bookkeeping inside the iterations
         const uint64_t dmask = __ballot(!have || done);
-        if (dmask != settled) {  // (wave-uniform)
+        if (next >= wend ? dmask == ~0ull : dmask != 0ull) {  // (wave-uniform)
         const bool gfin = have && (dmask & gmask) == gmask;
+        // attempt 0 failed or was handed over: phase 2 takes the target.  The ring positions of the
+        // wave's hand-overs come first, from one returning atomic issued by one lane: its wait then
+        // covers none of this pass's result stores (which it did when placed after them)
+        const bool handover = gfin && a.phase1 && res_att == INT_MAX;
+        uint32_t pos = 0;
+        if (a.phase1) {  // (uniform)
+            const uint64_t hmask = __ballot(handover);
+            if (hmask) {  // (uniform)
+                const int lead = __ffsll((unsigned long long)hmask) - 1;
+                uint32_t first = 0;
+                const uint32_t ring = (uint32_t)(wave % kIkSubRings);
+                if (lane == lead) first = atomicAdd(a.fail_ctl + ring * kIkCtlStride, (uint32_t)__popcll(hmask));
+                first = __shfl(first, lead);
+                pos = ring * (a.fail_mask + 1u) +
+                      ((first + (uint32_t)__popcll(hmask & ((1ull << lane) - 1ull))) & a.fail_mask);
+            }
+        }
         if (gfin) {
             const bool writer = (G > 1) ? ((gm != INT_MAX) ? (res_att == gm) : final_lane) : true;
-            if (a.phase1 && res_att == INT_MAX) {  // attempt 0 failed or was handed over: phase 2 takes it
-                const uint32_t pos = atomicAdd(&a.fail_ctl[0], 1u) & a.fail_mask;
+            if (handover) {
                 a.fail_list[pos] = (int32_t)i;
                 if (a.p1_cut) {  // hand-over state (see IkArgsT)
                     a.fail_aux[pos] = (int32_t)blk;
@@ -342,7 +380,12 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 if (base)
                     for (int k = 0; k < 3; ++k) KIN_IK_ST(q, P.base_col + k, ldq, off, b[k]);
                 if (iters) iters[i] = it;
-#if KINHIP_IK_SECT
+#if KINHIP_IK_SECT == 9
+                if constexpr (sizeof(T) == 4) {
+                    ep = __uint_as_float(rt_entry);
+                    er = __uint_as_float((uint32_t)__builtin_amdgcn_s_memrealtime());
+                }
+#elif KINHIP_IK_SECT
                 ep = (T)(double)sect_acc;
                 er = (T)(double)(ik_stamp() - sect_t0);
 #endif
@@ -357,8 +400,15 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         if (need && next < wend) {
             const uint64_t lead = 1ull << (grp * G);
             const int rank = __popcll(need & (lead - 1ull));
+            if (a.idx) {  // (uniform) phase 2: entry next + rank -> its ring (binary search over the prefix)
+                const uint32_t e = (uint32_t)(next + rank);
+                int r = 0;
+#pragma unroll
+                for (int step = kIkSubRings / 2; step >= 1; step >>= 1)
+                    if (__shfl(ring_excl, r + step) <= e) r += step;
+                rpos = (uint32_t)r * (a.fail_mask + 1u) + ((__shfl(ring_beg, r) + (e - __shfl(ring_excl, r))) & a.fail_mask);
+            }
             if (!have && (need & lead) && next + rank < wend) {
-                rpos = (fbeg + (uint32_t)(next + rank)) & a.fail_mask;
                 i = a.idx ? (int64_t)a.idx[rpos] : next + rank;
                 have = true;
                 start_target();  // the single (inlined) initialisation site
@@ -366,7 +416,6 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             next += __popcll(need);
         }
         if (__ballot(have) == 0) break;  // wave-uniform exit: range drained, every target written
-        settled = next >= wend ? __ballot(!have) : 0ull;
         }
         if (!have || done) continue;
 #if KINHIP_IK_SECT

@@ -76,10 +76,11 @@ struct IkArgs {
 // Device scratch of the two-phase IK schedule (launch_ik_dls): the list of targets attempt 0 did
 // not solve and its length, for batches of up to `cap` targets (null: single phase only)
 struct IkScratch {
-    int32_t* fail_list = nullptr;
+    int32_t* fail_list = nullptr;  // kIkSubRings rings of ring_cap entries (IkArgsT)
     int32_t* fail_aux = nullptr;   // per ring entry: the handed-over active set (IkArgsT::p1_cut)
-    uint32_t* fail_ctl = nullptr;  // 3 control words of the ring (IkArgsT), zero at allocation
-    int64_t cap = 0;               // ring entries, a power of two
+    uint32_t* fail_ctl = nullptr;  // per ring 3 control words on a 128-byte line, zero at allocation
+    int64_t cap = 0;               // targets per call the rings can take (a chunk of at most cap runs two-phase)
+    int64_t ring_cap = 0;          // entries per ring, a power of two
 };
 
 // true when some chunk of an n-target kin_ik_dls_batch call runs the two-phase schedule (only then

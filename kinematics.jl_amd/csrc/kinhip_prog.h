@@ -40,6 +40,10 @@ enum : int32_t { PF_JAC = 1, PF_WITH_ROT = 2, PF_RPY = 4, PF_ZERO = 8, PF_BASE =
 // The IK kernels take kIkChunk per launch.
 constexpr int64_t kChunk = int64_t(1) << 27;
 constexpr int64_t kIkChunk = kChunk / 8;
+// two-phase IK hand-over rings (IkArgsT, kinhip_ik_dev.h): one per lane of a wave (the phase-2 prefix
+// scan), their control words one 128-byte line apart
+constexpr int kIkSubRings = 64;
+constexpr int kIkCtlStride = 32;
 
 constexpr int kMaxChain = 32;  // phase-A steps (root -> spine link), register resident
 constexpr int kMaxJacCols = 64;
