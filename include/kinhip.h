@@ -260,8 +260,11 @@ typedef struct kin_ik_params {
                            sequential schedule's); only the parallelism changes.  With 0 and restarts,
                            batches of more than one round of waves (up to 2^20 targets) run in two
                            launches: attempt 0 of every target, then the remaining attempts of the
-                           targets attempt 0 did not solve, side by side (same results).  The two-phase
-                           scratch (first call: hipMalloc, synchronising) is per plan, with 4 sets used in
+                           targets attempt 0 did not solve, side by side (same results; a batch of one
+                           round hands attempt 0 over after 5/8 of its iterations and phase 2 resumes it
+                           beside the others, bit for bit).  The two-phase scratch (first call:
+                           hipMalloc of 8 sets of ~16 MiB, 64 hand-over rings each, synchronising) is
+                           per plan, with 4 sets used in
                            turn: calls on one stream are always safe; at most 4 calls of one plan may run
                            concurrently on different streams (a captured graph keeps the set of its
                            captured call).  Beyond that, pass lanes > 0 (one phase) or use one plan per
