@@ -155,7 +155,7 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=20, spec=1, dt=torch.float32)
            "dtype": "f32" if dt == torch.float32 else "f64",
            "params": "DLS lambda=1e-2, max_step=0.5, 64 iters incl. 3 seeded restarts, q0=0",
            "kernels": "specialised" if spec else "generic"}
-    if ctx.world > 1:
+    if ctx.dist is not None:  # (a group: world > 1, or the one-rank RCCL rehearsal)
         torch.cuda.synchronize()
         D.barrier(ctx)
         g0 = time.perf_counter()
@@ -206,7 +206,7 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
         if name == "min_dist":
             valid = (r[2] > 0).to(torch.uint8).reshape(1, -1)
             out[name]["valid_fraction"] = float(valid.float().mean())
-            if ctx.world > 1:
+            if ctx.dist is not None:
                 torch.cuda.synchronize()
                 D.barrier(ctx)
                 g0 = time.perf_counter()
@@ -489,7 +489,10 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="batch-size sweep, unpadded rows, strong scaling")
     args = ap.parse_args()
 
-    ctx = D.init_from_env()
+    # KINHIP_DIST_ALWAYS_GROUP=1 (torchrun --nproc-per-node 1): a one-rank RCCL group runs every
+    # collective of the sharded path -- barriers, max over ranks, the result gathers, the strong-scaling
+    # leg -- on the single-GPU box, exactly as each rank of an N-GPU run does
+    ctx = D.init_from_env(always_group=os.environ.get("KINHIP_DIST_ALWAYS_GROUP") == "1")
     rank, ws, dev = ctx.rank, ctx.world, ctx.device
     m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
     arm = [m.find_joint(n) for n in ARM]
@@ -570,6 +573,7 @@ def main():
                      "k_fk<float, 8>", "algorithmic_bytes_per_eval": bytes_per_eval,
                      "avg_launch_us": t_launch * 1e6},
     }
+    out["config"]["dist_backend"] = ctx.backend  # "nccl" = RCCL on ROCm; "none": one process, no group
     out["config"]["kernels"] = ("plan-specialised (kin_plan_specialize: program constants folded by hiprtc)"
                                 if headline_spec else "generic (program read from device memory)")
     if args.layout == "tiled":
@@ -642,7 +646,7 @@ def main():
                 sweep[f"2^{lg} {name}"] = {"evals_per_s": n_s * ws * k_s / ws_, "avg_launch_us": ds_ / k_s * 1e6,
                                            "achieved_GBs": bytes_per_eval * n_s / (ds_ / k_s) / 1e9}
         out["batch_sweep_fk_jac_f32"] = sweep
-    if ws > 1:  # strong scaling: one global 2^20 batch split across the ranks
+    if ctx.dist is not None:  # strong scaling: one global 2^20 batch split across the ranks
         st0, cnt = D.split_range(N, rank, ws)
         w_s, d_s = timed_leg(torch.float32, True, [gl], args.layout, n=cnt, start=st0)
         out["strong_scaling_fk_jac_f32"] = {"global_batch": N, "value": N * args.steps / w_s, "unit": "evals/s",

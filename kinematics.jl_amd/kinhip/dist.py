@@ -27,8 +27,10 @@ class Ctx:
     backend: str = "none"
 
 
-def init_from_env(backend: Optional[str] = None) -> Ctx:
-    """torchrun / torch.distributed.run environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+def init_from_env(backend: Optional[str] = None, always_group: bool = False) -> Ctx:
+    """torchrun / torch.distributed.run environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
+    `always_group`: create the process group even at world size 1 (the single-GPU test box runs the
+    RCCL collectives of the sharded path this way; a multi-rank RCCL group needs one GPU per rank)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -39,7 +41,7 @@ def init_from_env(backend: Optional[str] = None) -> Ctx:
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
     d, be = None, "none"
-    if world > 1:
+    if world > 1 or always_group:
         import torch.distributed as dist
         be = backend or ("nccl" if use_cuda else "gloo")
         if not dist.is_initialized():

@@ -88,3 +88,43 @@ def test_two_ranks_on_gpu_match_one_process():
         assert a.shape == b.shape, (name, a.shape, b.shape)
         np.testing.assert_array_equal(a, b, err_msg=name)
     assert (ref[1] <= 64).mean() > 0.99  # the IK set solves (kinhip.h: iters > max_iters = failure)
+
+
+def _rccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    import sys
+    sys.path.insert(0, ROOT)
+    try:
+        import bench
+        ctx = bench.D.init_from_env(backend="nccl", always_group=True)  # RCCL on ROCm
+        assert ctx.dist.get_backend() == "nccl", ctx.dist.get_backend()
+        res = _shard_results(ctx, bench)  # all_gather_into_tensor on device memory
+        mx = bench.D.max_over_ranks(ctx, [1.5, -2.0])  # all_reduce(MAX) of a device fp64 tensor
+        bench.D.barrier(ctx)
+        q.put(("ok", [r.numpy() for r in res], mx))
+        ctx.dist.destroy_process_group()
+    except Exception as e:
+        q.put(("error", repr(e), None))
+        raise
+
+
+def test_rccl_collectives_of_the_sharded_path():
+    """The RCCL ("nccl") backend itself: a one-rank group runs the bench's device-memory all-gathers,
+    the max-over-ranks all-reduce and the barrier; the gathered IK / collision results equal the
+    group-free run bit for bit.  (World size 1: the test box has one GPU.)"""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    p = mctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    status, payload, mx = q.get(timeout=110)
+    p.join(timeout=60)
+    assert status == "ok", payload
+    assert p.exitcode == 0, p.exitcode
+    assert mx == [1.5, -2.0]
+    ref = [r.numpy() for r in _shard_results(bench.D.init_from_env(), bench)]
+    for name, a, b in zip(("q", "iters", "err", "valid"), payload, ref):
+        np.testing.assert_array_equal(a, b, err_msg=name)
