@@ -168,7 +168,7 @@ def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=20, spec=1, dt=torch.float32)
     return out
 
 
-def _coll_leg(ctx, stream, n, steps, spec=1):
+def _coll_leg(ctx, stream, n, steps, spec=1, pad=256):
     """Config 5: FK + SDF validity samples of the planner (src/planning.jl collision check):
     Fetch arm (8 joints) with 14 build-defined spheres vs the 7-box fridge scene (door at 2.0 rad,
     base at (1.2, 0, 0)), `n` configurations per GPU, fp32.  Two kernels: min-distance only
@@ -181,19 +181,28 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
     if spec:
         _specialize(plan)
     Q = coll_shard(arm, ctx, n, dt)
+    # plain SoA rows padded to ld = n + pad like the FK legs (--row-pad): 2^20-element rows line the
+    # 134 row streams of a wave up on the same HBM channels (distances + gradients 104-105 -> 94-96 us,
+    # identical results; tools/coll_pad_ab.py, profiles/r03_coll_pad.txt)
+    ld = n + pad
+    Qb = torch.empty((8, ld), dtype=dt, device=ctx.device)
+    Qb[:, :n] = Q
+    Qp = Qb[:, :n]
+    Dp = torch.zeros((plan.n_sph, ld), dtype=dt, device=ctx.device)[:, :n]
+    Gp = torch.zeros((plan.n_sph, 8, ld), dtype=dt, device=ctx.device)[:, :, :n]
     out = {}
     for name, kw in (("min_dist", dict(dists=False, min_dist=True)),
-                     ("dists_grads", dict(dists=True, grads=True))):
+                     ("dists_grads", dict(dists=Dp, grads=Gp))):
         with torch.cuda.stream(stream):
             for _ in range(3):
-                r = plan.run(sdf, Q, stream=stream, **kw)
+                r = plan.run(sdf, Qp, stream=stream, **kw)
         torch.cuda.synchronize()
         D.barrier(ctx)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(stream)
         for _ in range(steps):
-            r = plan.run(sdf, Q, stream=stream, **kw)
+            r = plan.run(sdf, Qp, stream=stream, **kw)
         e1.record(stream)
         torch.cuda.synchronize()
         D.barrier(ctx)
@@ -202,7 +211,8 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
         nbytes = 8 * 4 + (4 if name == "min_dist" else ns * 4 + ns * 8 * 4)
         out[name] = {"value": n * ctx.world * steps / wall, "unit": "FK+SDF samples/s",
                      "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
-                     "achieved_GBs": nbytes * n / (dev_s / steps) / 1e9}
+                     "achieved_GBs": nbytes * n / (dev_s / steps) / 1e9,
+                     "layout": f"plain SoA rows, ld = n + {pad}"}
         if name == "min_dist":
             valid = (r[2] > 0).to(torch.uint8).reshape(1, -1)
             out[name]["valid_fraction"] = float(valid.float().mean())
@@ -266,7 +276,7 @@ def _coll_leg(ctx, stream, n, steps, spec=1):
             out[name]["layout"] = f"tiled SoA, tile {tile}"
     # ceilings of the distances + gradients legs (8 rows in, 14 + 112 rows out) from the same run
     for name, tl_ in (("dists_grads", 0), ("dists_grads_tiled", tile)):
-        pat_c = _pattern_us(8, ns + ns * 8, n, tl_, stream)
+        pat_c = _pattern_us(8, ns + ns * 8, n, tl_, stream, ld=0 if tl_ else ld)
         out[name]["pattern_ceiling_us"] = pat_c
         out[name]["frac_of_pattern"] = pat_c / out[name]["avg_launch_us"]
         out[name]["frac"] = out[name]["achieved_GBs"] / HBM_PEAK_GBS
@@ -418,24 +428,27 @@ def _pmc_traffic(workload, fname="pmc_fk_jac_f32.json"):
 _PROBE = None
 
 
-def _pattern_us(rows_in, rows_out, n, tile, stream, reps=20, warmup=3):
+def _pattern_us(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0):
     """The access pattern of a leg with no arithmetic (kinematics.jl_amd/lib/libkinprobe.so, a measurement
     probe built beside the engine): rows_in rows of q read and rows_out rows written per configuration,
-    fp32, tiled SoA (tile > 0) or plain rows (tile = 0), non-temporal stores like k_fk / k_coll.  Average
+    fp32, tiled SoA (tile > 0) or plain rows (tile = 0) `ld` >= n elements apart (0: ld = n), non-temporal
+    stores like k_fk / k_coll.  Average
     launch time (µs) from HIP events on `stream`: the leg's ceiling measured in the same run."""
     global _PROBE
     import ctypes as C
     if _PROBE is None:
         _PROBE = C.CDLL(os.path.join(ROOT, "kinematics.jl_amd", "lib", "libkinprobe.so"))
-        _PROBE.kinprobe_pattern.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
-        _PROBE.kinprobe_pattern.restype = C.c_int
-    ntot = -(-n // tile) * tile if tile else n
+        _PROBE.kinprobe_pattern_ld.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p,
+                                               C.c_void_p, C.c_void_p]
+        _PROBE.kinprobe_pattern_ld.restype = C.c_int
+    ld = tile if tile else (ld or n)
+    ntot = -(-n // tile) * tile if tile else ld
     q = torch.zeros(rows_in * ntot, dtype=torch.float32, device=stream.device)
     out = torch.zeros(rows_out * ntot, dtype=torch.float32, device=stream.device)
     st = stream.cuda_stream
 
     def launch():
-        rc = _PROBE.kinprobe_pattern(rows_in, rows_out, n, tile, q.data_ptr(), out.data_ptr(), st)
+        rc = _PROBE.kinprobe_pattern_ld(rows_in, rows_out, n, tile, ld, q.data_ptr(), out.data_ptr(), st)
         assert rc == 0, rc
     for _ in range(warmup):
         launch()
@@ -587,7 +600,7 @@ def main():
     if args.extras:
         out["roofline"]["torch_copy_GBs"] = _copy_bw(dev)  # context: torch device-to-device copy rate
         # the same bytes in the same layout with no kinematics (8 rows read, 60 written): this leg's ceiling
-        pat = _pattern_us(8, 60, N, args.tile if args.layout == "tiled" else 0, stream)
+        pat = _pattern_us(8, 60, N, args.tile if args.layout == "tiled" else 0, stream, ld=N + args.row_pad)
         out["roofline"]["pattern_ceiling"] = {"avg_launch_us": pat, "frac_of_pattern": pat / (t_launch * 1e6),
                                               "achieved_GBs": bytes_per_eval * N / pat / 1e3,
                                               "probe": "kinprobe_pattern(8 in, 60 out, same layout), same run"}
@@ -675,7 +688,7 @@ def main():
         out["config4_ik_dls"]["pmc"] = _pmc_valu("pmc_ik32s.json")
         out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
         out["config4_ik_dls_f64"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, dt=torch.float64)
-        out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec)
+        out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec, pad=args.row_pad)
         out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("pmc_coll32s.json")
         out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("pmc_collg32s.json")
         out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("pmc_collg32ts.json")

@@ -261,6 +261,11 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         ring_excl = inc - cnt;
         nt = (int64_t)__shfl(inc, kIkSubRings - 1);  // phase 2: the listed targets only
     }
+    if (chunk == 0) {  // phase 2 sized on the device: the listed targets over the launched waves
+        const int64_t nwav = ((int64_t)gridDim.x * blockDim.x) >> 6;
+        chunk = (nt + nwav - 1) / nwav;
+        if (chunk < 64 / G) chunk = 64 / G;
+    }
     const T* __restrict__ qin = a.q0 ? a.q0 : q;  // uniform: where the starting angles are read
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
     int64_t next = wbeg;  // wave-uniform: next unassigned target of this wave
@@ -634,7 +639,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 dq[s] = held ? T(0) : v;
                 // pushed further out of a limit it sits on (selects, no short-circuit branches)
                 const T out_lo = qs[s] <= S[s].lo ? -v : T(0), out_hi = qs[s] >= S[s].hi ? v : T(0);
-                nb |= (out_lo > T(0)) | (out_hi > T(0)) ? 1u << s : 0u;
+                nb |= ((out_lo > T(0)) | (out_hi > T(0))) ? 1u << s : 0u;
                 mx = fmax(mx, fabs(dq[s]));
             }
             blk = nb;

@@ -24,12 +24,18 @@ __global__ __launch_bounds__(256) void p_pattern(const float* __restrict__ q, fl
 
 }  // namespace
 
-extern "C" __attribute__((visibility("default"))) int kinprobe_pattern(int rows_in, int rows_out, int64_t n,
-                                                                       int64_t tile, const float* q, float* out,
-                                                                       void* stream) {
-    if (n <= 0 || rows_in < 0 || rows_out < 1 || tile < 0) return -1;
-    const int64_t ld = tile > 0 ? tile : n;
+// plain rows (tile = 0) ld elements apart (ld >= n: a padded row stride); tiled: ld is the tile
+extern "C" __attribute__((visibility("default"))) int kinprobe_pattern_ld(int rows_in, int rows_out, int64_t n,
+                                                                          int64_t tile, int64_t ld, const float* q,
+                                                                          float* out, void* stream) {
+    if (n <= 0 || rows_in < 0 || rows_out < 1 || tile < 0 || (tile > 0 ? ld != tile : ld < n)) return -1;
     hipLaunchKernelGGL(p_pattern, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, q, out, n,
                        rows_in, rows_out, tile, ld, ld);
     return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+extern "C" __attribute__((visibility("default"))) int kinprobe_pattern(int rows_in, int rows_out, int64_t n,
+                                                                       int64_t tile, const float* q, float* out,
+                                                                       void* stream) {
+    return kinprobe_pattern_ld(rows_in, rows_out, n, tile, tile > 0 ? tile : n, q, out, stream);
 }

@@ -1,0 +1,102 @@
+#!/bin/bash
+# The one GPU-box session driver (replaces the per-round r0N_*.sh scripts).  Every GPU step runs under
+# its own time limit and the script stops at the first failure; output goes under gpurun_out/.
+#   gpurun -- bash tools/gpu_session.sh <step> [<step> ...]
+# steps:
+#   tests[=<pytest selection>]  the GPU suite (default: tests/), -x, per-test timeout
+#   smoke                       __graft_entry__.smoke()
+#   bench                       python bench.py -> gpurun_out/bench.json
+#   bench-trace                 rocprofv3 --kernel-trace --stats of `bench.py --no-cpu` (gpurun_out/prof/bench)
+#   sweep                       python bench.py --no-cpu --sweep -> gpurun_out/bench_sweep.json
+#   rccl                        the RCCL test + the bench under a one-rank RCCL group (KINHIP_DIST_ALWAYS_GROUP=1)
+#   pmc=<tag>:<workload>[,...]  per workload a kernel trace + stats, then separate --pmc passes (never with
+#                               trace domains; each pass within the per-block counter limits); workloads of
+#                               tools/prof_kernel.py (e.g. fkjac32ts, ik32s, coll32s, collg32s, collg32ts)
+#   ik                          config-4 IK timing (product, twice) and 1M targets; per-iteration probe
+#   ik-sections                 iteration section stamps (A/B build, -DKINHIP_IK_SECT=k)
+#   ik-timeline                 per-lane entry / write timeline of one solve (A/B build)
+#   ik-dump                     the specialised IK source (A/B build, KINHIP_JIT_DUMP) + a kernel trace of config 4
+#   coll                        the plain-row padding A/B of the config-5 legs (tools/coll_pad_ab.py)
+#   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
+set -u -o pipefail
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+AB=$PWD/kinematics.jl_amd/lib/libkinhip_ab.so
+quiet() { grep -v "amdgpu.ids" || true; }
+
+pmc_run() {  # pmc_run <dir> <workload args> <rocprofv3 args...>
+  local d=$1 w=$2; shift 2
+  timeout -k 10 240 rocprofv3 "$@" --output-format csv -d gpurun_out/prof/$d -o $d -- python3 tools/prof_kernel.py $w \
+    > gpurun_out/prof_$d.log 2>&1
+  local rc=$?; echo "$d rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/prof_$d.log; exit $rc; }
+}
+
+for step in "$@"; do
+  echo "== $step"
+  case $step in
+    tests|tests=*)
+      sel=${step#tests}; sel=${sel#=}; sel=${sel:-tests}
+      timeout -k 10 1500 python -u -m pytest $sel -m gpu -x -v --timeout 300 --timeout-method thread \
+        > gpurun_out/gpu_tests.log 2>&1
+      rc=$?; tail -3 gpurun_out/gpu_tests.log
+      [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/gpu_tests.log | head -30; exit $rc; } ;;
+    smoke)
+      timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | quiet || exit 2 ;;
+    bench)
+      timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 3; }
+      cut -c1-400 gpurun_out/bench.json ;;
+    bench-trace)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/bench -o bench -- \
+        python3 bench.py --no-cpu > gpurun_out/bench_rocprof.log 2>&1 || { tail gpurun_out/bench_rocprof.log; exit 4; } ;;
+    sweep)
+      timeout -k 10 600 python bench.py --no-cpu --sweep --steps 20 > gpurun_out/bench_sweep.json \
+        2> gpurun_out/bench_sweep.err || { tail gpurun_out/bench_sweep.err; exit 5; } ;;
+    rccl)
+      timeout -k 10 240 python -u -m pytest tests/test_dist_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread \
+        > gpurun_out/rccl_tests.log 2>&1 || { tail -20 gpurun_out/rccl_tests.log; exit 6; }
+      tail -2 gpurun_out/rccl_tests.log
+      timeout -k 10 400 env KINHIP_DIST_ALWAYS_GROUP=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --no-cpu > gpurun_out/bench_rccl_1rank.json \
+        2> gpurun_out/bench_rccl_1rank.err || { tail gpurun_out/bench_rccl_1rank.err; exit 6; } ;;
+    pmc=*)
+      IFS=, read -ra specs <<< "${step#pmc=}"
+      for spec in "${specs[@]}"; do
+        IFS=: read -r TAG W EXTRA <<< "$spec"
+        WARGS="--what $W --steps 20 ${EXTRA:-}"
+        pmc_run ${TAG}_trace "$WARGS" --kernel-trace --stats
+        pmc_run ${TAG}_fetch "$WARGS" --pmc FETCH_SIZE
+        pmc_run ${TAG}_write "$WARGS" --pmc WRITE_SIZE
+        pmc_run ${TAG}_sq "$WARGS" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+        pmc_run ${TAG}_sq2 "$WARGS" --pmc SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_ANY \
+          SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INSTS_LDS
+        case $TAG in fk*)
+          pmc_run ${TAG}_mem "$WARGS" --pmc TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum GRBM_GUI_ACTIVE
+          pmc_run ${TAG}_tlb "$WARGS" --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+            TCP_UTCL1_REQUEST_sum GRBM_GUI_ACTIVE ;;
+        esac
+      done ;;
+    ik)
+      for r in 1 2; do timeout -k 10 120 env AB_SPEC=1 IK_N=65536 python -u tools/ik_ab.py 2>&1 | quiet || exit 8; done
+      timeout -k 10 120 env AB_SPEC=1 IK_N=1048576 AB_F32=1 python -u tools/ik_ab.py 2>&1 | quiet || exit 8
+      timeout -k 10 200 python -u tools/ik_iter_probe.py 2>&1 | quiet || exit 8 ;;
+    ik-sections)
+      for k in 1 2 3 4 5 6 7; do
+        timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=$k python -u tools/ik_sect.py 2>&1 | quiet || exit 8
+      done ;;
+    ik-timeline)
+      timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=9 python -u tools/ik_timeline.py 2>&1 | quiet || exit 8 ;;
+    ik-dump)
+      mkdir -p gpurun_out/jit gpurun_out/ikprof
+      timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DUMP=$PWD/gpurun_out/jit/ik AB_SPEC=1 AB_F32=1 IK_N=65536 \
+        python -u tools/ik_ab.py 2>&1 | quiet || exit 8
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ikprof -o ik -- python3 -u tools/ik_ab.py \
+        > gpurun_out/ikprof/run.log 2>&1 || exit 7 ;;
+    coll)
+      timeout -k 10 200 python -u tools/coll_pad_ab.py 2>&1 | quiet || exit 8 ;;
+    ab=*)
+      spec=${step#ab=}; w=${spec%%:*}; IFS=';' read -ra sets <<< "${spec#*:}"
+      timeout -k 10 900 python -u tools/ab.py $w "${sets[@]}" 2>&1 | quiet || exit 8 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
