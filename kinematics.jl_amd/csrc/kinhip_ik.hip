@@ -225,13 +225,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             const int na2 = natt - a2.att0;
             const int G2 = na2 <= 1 ? 1 : na2 <= 2 ? 2 : na2 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
-            // phase 2's grid: KINHIP_IK_P2_WAVES=<waves per CU> (A/B) launches that many waves and
-            // each sizes its share of the listed targets on the device (chunk 0); 0: one wave per
-            // 64 / G2 targets of the whole chunk, most of which find the list exhausted and exit
-            static const int p2w = ab_env_int("KINHIP_IK_P2_WAVES", 0);
-            const int64_t nw_all = (c + ng2 - 1) / ng2;
-            const int64_t nw2 = p2w > 0 ? std::min<int64_t>(nw_all, (int64_t)cus * p2w) : nw_all;
-            if ((e = one(a2, G2, s0, c, p2w > 0 ? 0 : ng2, nw2)) != hipSuccess) {
+            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
                 // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;
                 // the targets phase 1 did not solve keep undefined outputs (kin_ik_dls_batch says so)
                 (void)hipMemsetAsync(scr.fail_ctl, 0, sizeof(uint32_t) * kIkCtlStride * kIkSubRings, st);

@@ -225,6 +225,35 @@ __device__ __forceinline__ void ik_start_attempt(const KStep<T>* __restrict__ S,
     }
 }
 
+// inclusive prefix sum over the 64 lanes by DPP adds (row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast 15 / 31 across rows): six VALU instructions instead of six dependent ds_bpermute round trips
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    int t = (int)v;
+    t += __builtin_amdgcn_update_dpp(0, t, 0x111, 0xF, 0xF, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x112, 0xF, 0xF, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x114, 0xF, 0xF, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x118, 0xF, 0xF, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x142, 0xA, 0xF, false);
+    t += __builtin_amdgcn_update_dpp(0, t, 0x143, 0xC, 0xF, false);
+    return (uint32_t)t;
+}
+
+// min over the G lanes of an aligned lane group by DPP moves (quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror for 8-lane groups): VALU only, where __shfl_xor compiles to ds_bpermute, an LDS round
+// trip of ~100 cycles each, two per IK iteration at G = 4, in series, at one wave per SIMD
+template <int G>
+__device__ __forceinline__ int group_min(int v) {
+    if constexpr (G > 8) {
+#pragma unroll
+        for (int w = 1; w < G; w <<= 1) v = min(v, __shfl_xor(v, w, G));
+    } else {
+        if constexpr (G >= 2) v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));
+        if constexpr (G >= 4) v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));
+        if constexpr (G >= 8) v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false));
+    }
+    return v;
+}
+
 // Work distribution: wave w owns targets [w*chunk, (w+1)*chunk) and keeps its
 // 64/G lane groups busy: a group whose target is finished (all its lanes done)
 // writes the result and takes the wave's next target at once, so a wave no
@@ -248,23 +277,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     // before ring r (exclusive prefix over the rings); the wave's share is entries of that order
     uint32_t ring_beg = 0, ring_excl = 0;
     int64_t nt = n;
+    static_assert(kIkSubRings == 64, "one ring per lane of the phase-2 prefix");
     if (a.idx) {  // (uniform)
         const uint32_t* c = a.fail_ctl + lane * kIkCtlStride;
         ring_beg = c[1];
         const uint32_t cnt = c[0] - ring_beg;
-        uint32_t inc = cnt;
-#pragma unroll
-        for (int d = 1; d < kIkSubRings; d <<= 1) {
-            const uint32_t t = __shfl_up(inc, d);
-            if (lane >= d) inc += t;
-        }
+        const uint32_t inc = wave_incl_scan(cnt);
         ring_excl = inc - cnt;
-        nt = (int64_t)__shfl(inc, kIkSubRings - 1);  // phase 2: the listed targets only
-    }
-    if (chunk == 0) {  // phase 2 sized on the device: the listed targets over the launched waves
-        const int64_t nwav = ((int64_t)gridDim.x * blockDim.x) >> 6;
-        chunk = (nt + nwav - 1) / nwav;
-        if (chunk < 64 / G) chunk = 64 / G;
+        nt = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)inc, 63);  // phase 2: the listed targets only
     }
     const T* __restrict__ qin = a.q0 ? a.q0 : q;  // uniform: where the starting angles are read
     const int64_t wbeg = wave * chunk, wend = wbeg + chunk < nt ? wbeg + chunk : nt;
@@ -333,8 +353,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
     for (;;) {
         int gm = res_att;  // lowest converged attempt of this lane group's target so far
         if constexpr (G > 1) {
-#pragma unroll
-            for (int w = 1; w < G; w <<= 1) gm = min(gm, __shfl_xor(gm, w, G));
+            gm = group_min<G>(gm);  // (every lane of the wave is here: the loop only exits wave-wide)
             if (have && !done && gm < att) done = true;
         }
         // a group whose lanes are all done writes its target and takes the next one
@@ -405,13 +424,28 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         if (need && next < wend) {
             const uint64_t lead = 1ull << (grp * G);
             const int rank = __popcll(need & (lead - 1ull));
-            if (a.idx) {  // (uniform) phase 2: entry next + rank -> its ring (binary search over the prefix)
+            if (a.idx) {  // (uniform) phase 2: entry e = next + rank -> its ring (the last ring starting at or
+                // before e).  The wave's entries [e0, e1] span few rings: a uniform binary search (v_readlane)
+                // finds the ring of e0, then the lanes step over the rings that start inside (e0, e1]
                 const uint32_t e = (uint32_t)(next + rank);
-                int r = 0;
+                const uint32_t e0 = (uint32_t)next, e1 = (uint32_t)next + (uint32_t)__popcll(need) - 1u;
+                int r0 = 0;
 #pragma unroll
                 for (int step = kIkSubRings / 2; step >= 1; step >>= 1)
-                    if (__shfl(ring_excl, r + step) <= e) r += step;
-                rpos = (uint32_t)r * (a.fail_mask + 1u) + ((__shfl(ring_beg, r) + (e - __shfl(ring_excl, r))) & a.fail_mask);
+                    if ((uint32_t)__builtin_amdgcn_readlane((int)ring_excl, r0 + step) <= e0) r0 += step;
+                uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)ring_beg, r0);
+                uint32_t rx = (uint32_t)__builtin_amdgcn_readlane((int)ring_excl, r0);
+                int r = r0;
+                for (int rr = r0 + 1; rr < kIkSubRings; ++rr) {
+                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)ring_excl, rr);
+                    if (x > e1) break;  // (uniform)
+                    if (x <= e) {
+                        r = rr;
+                        rx = x;
+                        rb = (uint32_t)__builtin_amdgcn_readlane((int)ring_beg, rr);
+                    }
+                }
+                rpos = (uint32_t)r * (a.fail_mask + 1u) + ((rb + (e - rx)) & a.fail_mask);
             }
             if (!have && (need & lead) && next + rank < wend) {
                 i = a.idx ? (int64_t)a.idx[rpos] : next + rank;

@@ -481,6 +481,34 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
+def test_ik_dls_spec_two_phase_fp64_vs_oracle(dev, fetch_tree):
+    """Config 4's schedule in fp64 on the specialised kernels (two-phase with the hand-over; phase 2's
+    lane-group minimum, ring prefix and ring lookup by DPP / v_readlane): bit-identical to the one-phase
+    schedules of the same compilation (lanes 1 and 4) and to itself over repeated calls (the rings'
+    control words carry over), and the first 1,000 targets equal the oracle restatement (equal
+    iteration counts, angles to 1e-7)."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    ids = [j.id for j in arm]
+    om = O.OracleMech(fetch_tree)
+    N = 1 << 16
+    tgt = _targets(om, ids, gl.id, N, 58)
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
+    plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
+    T = torch.tensor(tgt, dtype=torch.float64, device=dev).contiguous()
+    kw = dict(max_iters=64, restarts=3, seed=7, lam=1e-2, max_step=0.5)
+    Z = torch.zeros((8, N), dtype=torch.float64, device=dev)
+    ref = plan.ik_dls(T, Z.clone(), lanes=0, **kw)
+    assert (ref[1] > 16).any()  # phase 2 did work
+    for lanes in (0, 0, 1, 4):
+        out = plan.ik_dls(T, Z.clone(), lanes=lanes, **kw)
+        assert all(torch.equal(a, b) for a, b in zip(out, ref)), lanes
+    k = 1000
+    rq, rit, _ = om.ik_dls_batch(np.zeros((8, k)), ids, gl.id, tgt[:, :k], **kw)
+    np.testing.assert_array_equal(ref[1][:k].cpu().numpy(), rit)
+    np.testing.assert_allclose(ref[0][:, :k].cpu().numpy(), rq, atol=1e-7)
+
+
 @pytest.mark.parametrize("dtype,N,lanes", [(torch.float32, 1 << 16, 0), (torch.float64, 1 << 16, 0),
                                              (torch.float32, 3000, 4), (torch.float64, 3000, 1)])
 def test_ik_dls_from_q0_identical(dev, dtype, N, lanes):

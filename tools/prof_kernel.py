@@ -84,9 +84,17 @@ elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge sce
         Qt = kinhip.tiled(Q, a.tile)
         for _ in range(a.steps):
             cp.run_tiled(sdf, Qt, a.n, dists=True, grads=True)
+    elif grads:  # rows padded like the bench's plain leg (ld = n + pad)
+        Qb = torch.empty((8, ld), dtype=dt, device=dev)
+        Qb[:, :a.n] = Q
+        Q = Qb[:, :a.n]
+        D = torch.zeros((cp.n_sph, ld), dtype=dt, device=dev)[:, :a.n]
+        G = torch.zeros((cp.n_sph, 8, ld), dtype=dt, device=dev)[:, :, :a.n]
+        for _ in range(a.steps):
+            cp.run(sdf, Q, dists=D, grads=G)
     else:
         for _ in range(a.steps):
-            cp.run(sdf, Q, dists=grads, grads=grads, min_dist=not grads)
+            cp.run(sdf, Q, dists=False, min_dist=True)
 else:
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     if SPEC:
