@@ -20,6 +20,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -283,6 +284,86 @@ def _coll_leg(ctx, stream, n, steps, spec=1, pad=256):
     out["tiled_vs_plain_dists_grads"] = out["dists_grads"]["avg_launch_us"] / out["dists_grads_tiled"]["avg_launch_us"]
     out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
                        f"samples sharded across ranks, {'specialised' if spec else 'generic'} kernels")
+    return out
+
+
+def _timed_calls(ctx, stream, fn, reps, warmup=2):
+    """(wall s, device s) of `reps` calls of fn on `stream`, bracketed by barrier + synchronize; max over
+    ranks.  Device time from HIP events on the launch stream."""
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            out = fn()
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    with torch.cuda.stream(stream):
+        for _ in range(reps):
+            out = fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    wall, dev_s = D.max_over_ranks(ctx, [time.perf_counter() - t0, e0.elapsed_time(e1) / 1e3])
+    return wall, dev_s, out
+
+
+def _scene_and_coll_ik_legs(ctx, stream, n, steps, spec=1):
+    """The two §8 f-rows beside config 5, fp32.
+    f2 `UnionSDF(mech)` (src/sdf.jl:14-32, 43-46, 82-97): the fridge's boxes attached to its links
+    (kin_sdf_create_attached), one door angle per sample -- fridge_demo.jl's sweep in one launch
+    (kin_coll_batch_scene: distances, 14x8 gradients and the minimum; door angle uniform in [0, 2.4],
+    fridge at (1.2, 0, 0)).
+    f3 bistage collision-aware IK (src/inverse_kinematics.jl:1-21): 4,096 targets per GPU in the open
+    fridge's upper compartment (x 0.9..1.05, y +-0.12, z 1.15..1.32, yaw +-0.3), one
+    CollisionIKPlan.solve = kin_ik_dls_batch_from + kin_ik_coll_batch (max_iters 128, 3 restarts,
+    margin 0.02, the reference's rpy objective)."""
+    dt = torch.float32
+    m, arm, sscc, sdf = fridge_scene()
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    plan = sscc.plan(arm, dtype=dt)
+    if spec:
+        _specialize(plan)
+    Q = coll_shard(arm, ctx, n, dt, seed=556)
+    g = torch.Generator().manual_seed(90 + ctx.rank)
+    SQ = torch.zeros((4, n), dtype=torch.float64)
+    SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
+    SQ[1] = 1.2
+    SQ = SQ.to(dt).to(ctx.device).contiguous()
+    wall, dev_s, r = _timed_calls(ctx, stream, lambda: plan.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ,
+                                                                stream=stream), steps)
+    ns = plan.n_sph
+    nbytes = (8 + 4) * 4 + ns * 4 + ns * 8 * 4 + 4  # q + scene columns in; distances, gradients, minimum out
+    out = {"f2_scene_door_sweep": {"value": n * ctx.world * steps / wall, "unit": "FK+SDF samples/s",
+                                   "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
+                                   "achieved_GBs": nbytes * n / (dev_s / steps) / 1e9,
+                                   "valid_fraction": float((r[2] > 0).float().mean()),
+                                   "kernel": "kinhip_jit_colls_1 (specialised)" if spec else "k_coll_scene"}}
+    gl = m.find_link("gripper_link")
+    nt = 4096
+    rng = np.random.default_rng(17 + ctx.rank)
+    tg = np.zeros((12, nt))
+    for k in range(nt):
+        x, y, z, yaw = rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32), rng.uniform(-0.3, 0.3)
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        R = np.array([[c, -s_, 0.0], [s_, c, 0.0], [0.0, 0.0, 1.0]])
+        tg[:, k] = np.concatenate([R.T.reshape(-1), [x, y, z]])
+    tg = torch.tensor(tg, dtype=dt, device=ctx.device).contiguous()
+    cplan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dt)
+    if spec:
+        _specialize(cplan)
+    Q0 = torch.zeros((8, nt), dtype=dt, device=ctx.device)
+    reps = 5
+    wall, dev_s, (Qs, it, err) = _timed_calls(
+        ctx, stream, lambda: cplan.solve(sdf, tg, Q0, max_iters=128, restarts=3, seed=1, index_base=ctx.rank * nt,
+                                         stream=stream), reps, warmup=1)
+    conv = it <= 128
+    out["f3_collision_ik"] = {"value": nt * ctx.world * reps / wall, "unit": "bistage IK solves/s",
+                              "targets_per_gpu": nt, "ms_per_batch": dev_s / reps * 1e3,
+                              "converged": float(conv.float().mean()),
+                              "min_sphere_distance_converged": float(err[2][conv].min()) if bool(conv.any()) else None,
+                              "kernels": "specialised" if spec else "generic"}
     return out
 
 
@@ -692,6 +773,7 @@ def main():
         out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("pmc_coll32s.json")
         out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("pmc_collg32s.json")
         out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("pmc_collg32ts.json")
+        out.update(_scene_and_coll_ik_legs(ctx, stream, N, max(5, args.steps // 2), spec=args.spec))
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
         if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)
             out["generic_kernels"] = {

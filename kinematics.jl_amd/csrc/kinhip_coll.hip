@@ -18,7 +18,8 @@ __global__ __launch_bounds__(256) void k_coll(const KProg<T> P, const KStep<T>* 
     coll_body<T, MAXA, GRAD>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem);
 }
 
-// the same with the union's boxes attached to a scene mechanism (kin_coll_batch_scene; generic only)
+// the same with the union's boxes attached to a scene mechanism (kin_coll_batch_scene; the plan-specialised
+// form is kinhip_jit_colls_*, kinhip_jit.cpp)
 template <typename T, int MAXA, bool GRAD>
 __global__ __launch_bounds__(256) void k_coll_scene(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                     const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
@@ -35,7 +36,8 @@ __global__ __launch_bounds__(256) void k_coll_scene(const KProg<T> P, const KSte
 template <typename T>
 hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                              const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
-                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st) {
+                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf,
+                             hipStream_t st) {
     const Tiling tl{0xffffffffu, 0, 0, 0, 0};
     const size_t lds = grads && a.n_boxes <= kCollLdsBoxes ? (size_t)a.n_boxes * sizeof(KBox<T>) : 0;
     for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
@@ -53,6 +55,17 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
         T* dc = dists ? dists + s0 : dists;
         T* gc = grads ? grads + s0 : grads;
         T* mc = min_dist ? min_dist + s0 : min_dist;
+        if (jf && jf->coll_scene[grads ? 1 : 0]) {  // plan-specialised (kin_plan_specialize, KIN_SPEC_COLL)
+            int64_t cc = c;
+            CollArgs ac = a;
+            Tiling tc = tl;
+            void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc, (void*)&ldd,
+                            (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tc, (void*)&sa};
+            const hipError_t e = hipModuleLaunchKernel(jf->coll_scene[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1,
+                                                       (unsigned)lds, st, args, nullptr);
+            if (e != hipSuccess) return e;
+            continue;
+        }
 #define KIN_COS_LAUNCH(MA) \
         hipLaunchKernelGGL((k_coll_scene<T, MA, false>), grid, block, lds, st, P, steps, sph, boxes, a, qc, ldq, c, dc, ldd, gc, ldg, mc, tl, sa)
 #define KIN_COSG_LAUNCH(MA) \
@@ -122,7 +135,8 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
                                        int64_t, T*, int64_t, T*, const TileArgs&, const JitFns*, hipStream_t); \
     template hipError_t launch_coll_scene<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, \
                                              const LaunchGeom&, const CollArgs&, const SceneLaunch&, const T*,        \
-                                             int64_t, int64_t, T*, int64_t, T*, int64_t, T*, hipStream_t);
+                                             int64_t, int64_t, T*, int64_t, T*, int64_t, T*, const JitFns*,     \
+                                             hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

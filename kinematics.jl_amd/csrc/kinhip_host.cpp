@@ -1588,9 +1588,16 @@ int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncatio
     if (const int rc = check_device(sdf->device, "kin_coll_batch_scene", "the kin_sdf")) return rc;
     CollArgs a = coll_args(sdf, truncation, 0.0);
     const size_t np = p->parts.empty() ? 1 : p->parts.size();
+    // the specialised kernels' soffset row addressing (as coll_launch): every row offset plus the lane
+    // span below 2^31 bytes, else the generic kernels
+    const int64_t esz = p->dtype == KIN_F32 ? 4 : 8, span = std::min<int64_t>(n, kChunk);
+    const auto fits = [&](int64_t rows, int64_t ld) { return ((rows + 1) * ld + span) * esz < (int64_t(1) << 31); };
+    const bool soff = fits(p->nqcols, ldq) && (!dists || fits(p->n_sph, ldd)) &&
+                      (!grads || fits((int64_t)p->n_sph * p->nqcols, ldg));
     for (size_t k = 0; k < np; ++k) {
         const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
         a.accumulate = k > 0;
+        const JitFns* jf = soff ? jit_fns(s->jit) : nullptr;
         const void* sc = s->dtype == KIN_F32 ? sdf->d_scene_f32 : sdf->d_scene_f64;
         const SceneLaunch sl{sc, (const char*)sc + sdf->scene_steps_off, scene_q, lds, sdf->n_groups,
                              sdf->scene_base_col, lds == 0 ? 1 : 0};
@@ -1598,11 +1605,12 @@ int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncatio
         if (s->dtype == KIN_F32)
             e = launch_coll_scene<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
                                          (const KBox<float>*)sdf->d_f32, s->geom, a, sl, (const float*)q, ldq, n,
-                                         (float*)dists, ldd, (float*)grads, ldg, (float*)min_dist, (hipStream_t)stream);
+                                         (float*)dists, ldd, (float*)grads, ldg, (float*)min_dist, jf,
+                                         (hipStream_t)stream);
         else
             e = launch_coll_scene<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
                                           (const KBox<double>*)sdf->d_f64, s->geom, a, sl, (const double*)q, ldq, n,
-                                          (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist,
+                                          (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, jf,
                                           (hipStream_t)stream);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll_scene launch: ") + hipGetErrorString(e));
     }

@@ -54,6 +54,7 @@ struct JitFns {
     hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
+    hipFunction_t coll_scene[2] = {};  // the same over a union attached to a scene (kin_coll_batch_scene)
     hipFunction_t ikc[2] = {};    // collision-aware IK [rows == 6]
 };
 
@@ -129,7 +130,7 @@ struct SceneLaunch {
 template <typename T>
 hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                              const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
-                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, hipStream_t st);
+                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st);
 
 template <typename T>
 hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,

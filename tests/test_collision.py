@@ -387,6 +387,35 @@ def test_gpu_collision_specialized_equals_generic(dtype, with_base):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+def test_gpu_attached_scene_specialized_equals_generic(dtype, with_base):
+    """The plan-specialised scene kernels (kinhip_jit_colls_*: the arm chain and spheres as constants,
+    the scene's groups and boxes as data) == the generic k_coll_scene: distances, gradients and minimum
+    over per-sample door angles and moved fridges, and over one scene state for the whole launch."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(with_base)
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    sdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    N = 3000
+    g = torch.Generator().manual_seed(12)
+    nq = 8 + (3 if with_base else 0)
+    Q = (torch.rand((nq, N), generator=g, dtype=torch.float64) * 2.4 - 1.2).to(dtype).to(dev)
+    SQ = torch.stack([torch.rand(N, generator=g, dtype=torch.float64) * 2.4,
+                      1.1 + 0.2 * torch.rand(N, generator=g, dtype=torch.float64),
+                      0.1 * torch.rand(N, generator=g, dtype=torch.float64) - 0.05,
+                      0.4 * torch.rand(N, generator=g, dtype=torch.float64) - 0.2]).to(dtype).to(dev).contiguous()
+    gen = sscc.plan(arm, dtype=dtype)
+    spe = sscc.plan(arm, dtype=dtype).specialize()
+    assert spe.specialized == kinhip.KIN_SPEC_COLL
+    for sq in (SQ, SQ[:, 7].contiguous()):
+        for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True)):
+            for x, y in zip(gen.run(sdf, Q, scene_q=sq, **kw), spe.run(sdf, Q, scene_q=sq, **kw)):
+                assert (x is None and y is None) or torch.equal(x, y), kw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("spec", [False, True])
 def test_gpu_collision_broad_phase_exact(dtype, spec):
     """Finite truncation enables the broad phase (spheres provably beyond truncation + the union's
