@@ -386,7 +386,10 @@ typedef struct kin_ik_coll_params {
  * q0 ([n_q(+3)][ldq], read; q0 == q is in place) damped Gauss-Newton steps on the pose residual of
  * kin_ik_params.with_rot (2 = the reference's rpy objective) plus one-sided penalty rows
  * a_k = grad sdf^T J_k of the spheres inside the band, normal equations over the q joints (+ base),
- * joint limits by an active set and a clamp; restarts as in kin_ik_dls_batch (lanes ignored, lambda > 0).
+ * joint limits by an active set and a clamp; restarts as in kin_ik_dls_batch (lambda > 0).  lanes: 0 = auto
+ * (4 lanes per target running the attempts side by side for batches of at most 65,536 targets with
+ * restarts, else 1), 1 = one lane per target (attempts in sequence), 2 / 4 / 8 = the 4-lane form;
+ * identical results for every setting.
  * Converged (iters <= max_iters, else max_iters + 1) when |dp| < tol_pos, |rot| < tol_rot and every
  * sphere has d >= margin - feas.  err: [3][lde] |dp|, |rot err|, min sphere distance (or NULL). */
 KINHIP_API int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,

@@ -66,6 +66,10 @@ __device__ __noinline__ void sincos_slow(double x, double* s, double* c) { sinco
 
 __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
     if (__builtin_expect(!(fabsf(x) < 8192.0f), 0)) {
+        if (!isfinite(x)) {  // NaN / inf -> NaN, in line: no out-of-line call for a diverged lane
+            *s = *c = x - x;
+            return;
+        }
         sincos_slow(x, s, c);
         return;
     }
@@ -84,6 +88,10 @@ __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
 
 __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
     if (__builtin_expect(!(fabs(x) < 1048576.0), 0)) {
+        if (!isfinite(x)) {  // NaN / inf -> NaN, in line: no out-of-line call for a diverged lane
+            *s = *c = x - x;
+            return;
+        }
         sincos_slow(x, s, c);
         return;
     }

@@ -1483,8 +1483,10 @@ int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params
         return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad IK parameters (lambda must be > 0)");
     if (!std::isfinite(cp->margin) || !(cp->band >= 0) || !(cp->weight > 0) || !(cp->feas >= 0))
         return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad collision parameters");
+    if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
+        return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
     const IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-                   prm->restarts, prm->seed, 1, prm->index_base};
+                   prm->restarts, prm->seed, prm->lanes, prm->index_base};
     const IkcArgs c{cp->margin, cp->band, cp->weight, cp->feas};
     const CollArgs ca{INFINITY, 0.0, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
                       {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
     nakamura_body<T, MAXA>(P, S, pts, ldpt, q, ldq, n);
 }
 
-template <typename T, int MAXA, int ROWS>
+template <typename T, int MAXA, int ROWS, int G>
 __global__ __launch_bounds__(64) void k_ik_coll(const KProg<T> P, const KStep<T>* __restrict__ S,
                                                 const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                                 const CollArgs ca, const IkcArgsT<T> cz, const IkArgsT<T> a,
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) void k_ik_coll(const KProg<T> P, const KStep<T>
                                                 int64_t n, int32_t* __restrict__ iters, T* __restrict__ err,
                                                 int64_t lde) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ikc_body<T, MAXA, ROWS>(P, S, sph, boxes, ca, cz, a, tgt, ldt, q, ldq, n, iters, err, lde, smem);
+    ikc_body<T, MAXA, ROWS, G>(P, S, sph, boxes, ca, cz, a, tgt, ldt, q, ldq, n, iters, err, lde, smem);
 }
 
 }  // namespace
@@ -244,8 +244,21 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     return hipSuccess;
 }
 
-// k_ik_coll: one target per lane, 64-lane workgroups (a few thousand targets still spread over
-// many CUs); the union's boxes in LDS for the argmin gathers (k_coll)
+// Lanes per k_ik_coll target: 4 (attempts side by side, ikc_body) in the plan-specialised kernels while
+// the batch is small enough that the lanes would idle otherwise (<= 65,536 targets, the ik_group rule)
+// and the schedule has at least 4 attempts, else 1; kin_ik_params.lanes = 1 forces one lane, 2 / 4 / 8
+// ask for the 4-lane form.  Identical results.  The generic kernels keep one lane per target: their fp64
+// 4-lane instantiation (~500 registers, SGPR spills, an out-of-line sincos call) faulted once on the GPU
+// (illegal address, with idle fourth lanes at 3 attempts; profiles/r03_ikc_lanes.txt), cause not found.
+static int ikc_group(int64_t n, int natt, int lanes, bool spec) {
+    static const int env = ab_env_int("KINHIP_IKC_GROUP", 0);
+    const int forced = lanes ? lanes : env;
+    if (!spec || natt < kIkcLanes || forced == 1) return 1;
+    return forced > 1 || n * 8 <= (int64_t(1) << 19) ? kIkcLanes : 1;
+}
+
+// k_ik_coll: G lanes per target (ikc_group), 64-lane workgroups (a few thousand targets still spread
+// over many CUs); the union's boxes in LDS for the argmin gathers (k_coll)
 template <typename T>
 hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                           const LaunchGeom& g, const CollArgs& ca, const IkcArgs& c, const IkArgs& a, const T* target,
@@ -257,6 +270,7 @@ hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSpher
                   0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
     const IkcArgsT<T> cz{T(c.margin), T(c.band), T(c.weight), T(c.feas)};
     const size_t lds = ca.n_boxes <= kCollLdsBoxes ? (size_t)ca.n_boxes * sizeof(KBox<T>) : 0;
+    const int G = ikc_group(n, natt, a.lanes, jf && jf->ikc[a.with_rot ? 1 : 0][1]);
     for (int64_t s0 = 0; s0 < n; s0 += kIkChunk) {
         const int64_t cn = std::min(kIkChunk, n - s0);
         at.ibase = a.index_base + s0;
@@ -265,8 +279,8 @@ hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSpher
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
-        const unsigned grid = (unsigned)((cn + 63) / 64);
-        const hipFunction_t jk = jf ? jf->ikc[a.with_rot ? 1 : 0] : nullptr;
+        const unsigned grid = (unsigned)((cn * G + 63) / 64);
+        const hipFunction_t jk = jf ? jf->ikc[a.with_rot ? 1 : 0][G > 1 ? 1 : 0] : nullptr;
         if (jk) {
             int64_t cc = cn;
             CollArgs cac = ca;
@@ -278,7 +292,7 @@ hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSpher
             continue;
         }
 #define KIN_IKC(MA, R) \
-        hipLaunchKernelGGL((k_ik_coll<T, MA, R>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, tc, ldt, qc, ldq, cn, ic, ec, lde)
+        hipLaunchKernelGGL((k_ik_coll<T, MA, R, 1>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, tc, ldt, qc, ldq, cn, ic, ec, lde)
         if (g.maxA == 4) {
             if (a.with_rot) KIN_IKC(4, 6); else KIN_IKC(4, 3);
         } else if (g.maxA == 8) {

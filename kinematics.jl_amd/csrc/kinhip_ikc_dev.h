@@ -19,7 +19,13 @@ struct IkcArgsT {
     T feas;    // converged only when every sphere has d >= margin - feas
 };
 
-// One lane per target, attempts in sequence (the restart schedule of k_ik_dls, G = 1).  Per iteration:
+// G lanes per target (aligned lane groups, G = 1 or 4): lane `slot` of a group runs attempts slot,
+// slot + G, ... of the restart schedule of k_ik_dls side by side with the others, stops once a lower
+// attempt of its target has converged (group_min by DPP every iteration), and the lowest converged
+// attempt (else the last one) writes.  Every lane's arithmetic is the sequential schedule's (G = 1:
+// attempts in sequence on one lane), so the results are identical for G = 1 and 4; a small batch (the
+// bistage solve's few thousand targets are a fraction of a wave per SIMD) gains the parallelism and
+// a wave no longer lasts as long as the sum of its slowest target's attempts.  Per iteration:
 // FK with the joint records, every sphere's centre and UnionSDF distance + analytic gradient on the
 // way (k_coll's union_sdf), then ONE damped Gauss-Newton step on the normal equations over the chain's
 // joints (+ base):
@@ -31,7 +37,7 @@ struct IkcArgsT {
 // sphere has d >= margin - feas.  Joint limits: a joint that sits on a limit and is pushed further out
 // (by this step if it was free, by the gradient J^T e + ... if it was held) is held out of the next
 // step (row / column of the system replaced by the identity); q is clamped to the limits.
-template <typename T, int MAXA, int ROWS>
+template <typename T, int MAXA, int ROWS, int G>
 __device__ __forceinline__ void ikc_body(const KProg<T>& P, const KStep<T>* __restrict__ S,
                                          const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                          const CollArgs& ca, const IkcArgsT<T>& cz, const IkArgsT<T>& a,
@@ -45,8 +51,10 @@ __device__ __forceinline__ void ikc_body(const KProg<T>& P, const KStep<T>* __re
             reinterpret_cast<uint4*>(smem)[w] = reinterpret_cast<const uint4*>(boxes)[w];
         __syncthreads();
     }
-    const uint64_t gi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gi >= (uint64_t)n) return;
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lane groups inside a DPP row");
+    const uint64_t gi = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int slot = (int)(threadIdx.x % G);
+    if (gi >= (uint64_t)n) return;  // (whole lane groups: blockDim is a multiple of G)
     const uint32_t off = (uint32_t)gi * (uint32_t)sizeof(T);
     const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + ca.n_boxes);
     const bool base = (P.flags & PF_BASE) != 0;
@@ -68,15 +76,26 @@ __device__ __forceinline__ void ikc_body(const KProg<T>& P, const KStep<T>* __re
     if (base)
         for (int k = 0; k < 3; ++k) b0[k] = ld_soa(qin, P.base_col + k, ldq, off);
     T qs[MAXA], b[3] = {b0[0], b0[1], b0[2]};
-    ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + (int64_t)gi, 0, qs);
     const int L = a.attempt_len;
+    // this lane's first attempt: attempt 0 from q0 at iteration 0, attempt k >= 1 re-drawn at kL + 1
+    int att = slot, it = slot > 0 ? slot * L + 1 : 0;
+    ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
     uint32_t held = 0;  // bit v: variable v (step v, base MAXA + k) held out of the step
-    int att = 0, it = 0;
-    bool conv = false;
+    bool conv = false, final_lane = false;
+    bool done = att >= a.n_attempts;  // (lanes beyond the schedule's attempts)
+    int res_att = INT_MAX;            // this lane's converged attempt
     T ep = T(0), er = T(0), dmin = T(INFINITY);
     const T w2 = cz.weight * cz.weight;
     const T act = cz.margin + cz.band;
     for (;;) {
+        if constexpr (G > 1) {  // every lane of the wave is here: the loop exits wave-wide
+            const int gm = group_min<G>(res_att);  // lowest converged attempt of the target so far
+            if (!done && gm < att) done = true;
+            if (__ballot(!done) == 0) break;
+        } else {
+            if (done) break;
+        }
+        if (done) continue;
         // ---- FK, records, spheres -------------------------------------------------------------
         Fr<T> f;
         if (base) base_frame(f, b[0], b[1], b[2]);
@@ -167,11 +186,22 @@ __device__ __forceinline__ void ikc_body(const KProg<T>& P, const KStep<T>* __re
         }
         if (ep < a.tol_pos && er < a.tol_rot && dmin >= cz.margin - cz.feas) {
             conv = true;
-            break;
+            res_att = att;
+            done = true;
+            continue;
         }
-        if (it >= a.max_iters) break;
-        if (L > 0 && it > 0 && it % L == 0) {  // attempt over: the next one, re-drawn
-            if (++att >= a.n_attempts) break;
+        if (it >= a.max_iters) {  // (only the last attempt gets here)
+            final_lane = true;
+            done = true;
+            continue;
+        }
+        if (L > 0 && it > 0 && it % L == 0) {  // attempt over: this lane's next one, re-drawn
+            att += G;
+            if (att >= a.n_attempts) {
+                final_lane = att - G == a.n_attempts - 1;
+                done = true;
+                continue;
+            }
             it = att * L + 1;
             ik_start_attempt<T, MAXA>(S, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
             b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
@@ -305,7 +335,11 @@ __device__ __forceinline__ void ikc_body(const KProg<T>& P, const KStep<T>* __re
             for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * y[MAXA + k];
         ++it;
     }
-    // ---- outputs ----------------------------------------------------------------------------------
+    // ---- outputs: the lowest converged attempt of the target, else the last one --------------------
+    if constexpr (G > 1) {
+        const int gm = group_min<G>(res_att);
+        if (gm != INT_MAX ? res_att != gm : !final_lane) return;
+    }
 #pragma unroll
     for (int s = 0; s < MAXA; ++s) {
         const int32_t c = S[s].qcol;

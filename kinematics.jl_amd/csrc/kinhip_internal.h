@@ -55,7 +55,7 @@ struct JitFns {
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
     hipFunction_t coll_scene[2] = {};  // the same over a union attached to a scene (kin_coll_batch_scene)
-    hipFunction_t ikc[2] = {};    // collision-aware IK [rows == 6]
+    hipFunction_t ikc[2][2] = {};  // collision-aware IK [rows == 6][kIkcLanes lanes per target]
 };
 
 // jf: the plan-specialised kernels (kinhip_jit.cpp) or null for the generic one

@@ -40,6 +40,8 @@ enum : int32_t { PF_JAC = 1, PF_WITH_ROT = 2, PF_RPY = 4, PF_ZERO = 8, PF_BASE =
 // The IK kernels take kIkChunk per launch.
 constexpr int64_t kChunk = int64_t(1) << 27;
 constexpr int64_t kIkChunk = kChunk / 8;
+// lanes per target of the parallel-attempt collision-aware IK kernel (k_ik_coll, ikc_group)
+constexpr int kIkcLanes = 4;
 // two-phase IK hand-over rings (IkArgsT, kinhip_ik_dev.h): one per lane of a wave (the phase-2 prefix
 // scan), their control words one 128-byte line apart
 constexpr int kIkSubRings = 64;

@@ -280,9 +280,11 @@ class CollisionIKPlan(Plan):
 
     def ik_coll(self, sdf: UnionSDF, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
                 margin=0.02, band=0.0, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-                max_step=0.5, with_rot=2, restarts=0, seed=0, index_base=0, stream=None):
+                max_step=0.5, with_rot=2, restarts=0, seed=0, lanes=0, index_base=0, stream=None):
         """Stage 2 alone (kin_ik_coll_batch): from Q0 (or Q in place) -> (Q, iters [N], err [3, N]:
-        |dp|, |rot|, min sphere distance).  iters > max_iters: not converged."""
+        |dp|, |rot|, min sphere distance).  iters > max_iters: not converged.  `lanes`: 0 = auto (restart
+        attempts side by side on 4 lanes per target for small batches), 1 = attempts in sequence on one
+        lane; the results do not depend on it."""
         N = self._check_q(Q)
         _plan_device(sdf, Q)
         if Q0 is not None:
@@ -295,7 +297,7 @@ class CollisionIKPlan(Plan):
         iters = torch.empty(N, dtype=torch.int32, device=Q.device)
         err = torch.empty((3, N), dtype=self.dtype, device=Q.device)
         prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
-                         int(restarts), int(seed), 0, int(index_base))
+                         int(restarts), int(seed), int(lanes), int(index_base))
         cp = K.IkCollParams(float(margin), float(band), float(weight), float(feas))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,

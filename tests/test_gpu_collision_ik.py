@@ -253,3 +253,45 @@ def test_collision_ik_iterates_vs_oracle(spec):
     np.testing.assert_array_equal(it, rit)
     np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
     np.testing.assert_allclose(err.cpu().numpy(), rerr, atol=1e-9)
+
+
+@pytest.mark.parametrize("spec", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_collision_ik_lanes_identical(spec, dtype):
+    """kin_ik_coll_batch runs the restart attempts of a target side by side on 4 lanes (specialised
+    kernels, >= 4 attempts, auto for small batches) or in sequence on one lane (lanes = 1): every lane's
+    arithmetic is the sequential schedule's, so angles, iteration counts and errors are bit-identical --
+    out of place and in place, with 4 attempts (one per lane) and 5 (lane 0 runs attempts 0 and 4);
+    the generic kernels (one lane per target whatever `lanes` says) give the same answers."""
+    m, arm, sscc, sdf = _scene()
+    gl = m.find_link("gripper_link")
+    dev = torch.device("cuda", 0)
+    N = 1500  # not a multiple of the wave's 16 lane groups
+    rng = np.random.default_rng(29)
+    tg = np.zeros((12, N))
+    for k in range(N):
+        T = _pose((rng.uniform(0.85, 1.1), rng.uniform(-0.15, 0.15), rng.uniform(1.1, 1.35)), rng.uniform(-0.4, 0.4))
+        tg[:, k] = np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+    tgt = torch.tensor(tg, dtype=dtype, device=dev).contiguous()
+    plan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dtype)
+    if spec:
+        plan.specialize()
+    Q0 = torch.zeros((8, N), dtype=dtype, device=dev)
+    Q1 = torch.empty_like(Q0)
+    plan.ik_dls(tgt, Q1, Q0=Q0, max_iters=64, restarts=3, seed=2, with_rot=2)
+    for restarts, max_iters in ((3, 96), (4, 100)):
+        kw = dict(margin=0.02, band=0.01, max_iters=max_iters, tol_pos=1e-4, tol_rot=1e-4, with_rot=2,
+                  restarts=restarts, seed=7)
+        ref = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=1, **kw)
+        for lanes in (0, 4):
+            got = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, **kw)
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b), (restarts, lanes)
+        Qi = Q1.clone()
+        got = plan.ik_coll(sdf, tgt, Qi, lanes=0, **kw)  # in place
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), (restarts, "in place")
+        it = ref[1].cpu().numpy()
+        # the case exercises the schedule: targets solved in attempt 0, in a restart, and not at all
+        L = max_iters // (restarts + 1)
+        assert (it <= L).any() and ((it > L) & (it <= max_iters)).any(), np.bincount(np.minimum(it, max_iters + 1))

@@ -10,7 +10,7 @@ The product library libkinhip.so never reads these variables (kinhip_internal.h 
          python tools/ab.py coll base "KINHIP_JIT_DEFS=-DKINHIP_AABB_UNROLL=1" KINHIP_COLL_FAST_TRIG=0
 
 Knobs (all read only by the A/B build): KINHIP_IK_GROUP, KINHIP_IK_RESIDENT, KINHIP_IK_QUEUE,
-KINHIP_IK_TWO_PHASE, KINHIP_IK_TP_QUEUE (IK schedule), KINHIP_FK_PER_LANE (FK grid), KINHIP_JIT_IK_WAVES,
+KINHIP_IK_TWO_PHASE, KINHIP_IK_TP_QUEUE (IK schedule), KINHIP_IKC_GROUP (collision-aware IK lanes), KINHIP_FK_PER_LANE (FK grid), KINHIP_JIT_IK_WAVES,
 KINHIP_JIT_COLL_WAVES (occupancy), KINHIP_COLL_FAST_TRIG, KINHIP_IK_FAST_ATAN (arithmetic variants),
 KINHIP_JIT_SLP, KINHIP_JIT_DEFS, KINHIP_JIT_OPTS (compiler options / definitions), KINHIP_JIT_DUMP
 (keep the generated source).  Every run prints its workload's own result line prefixed by the setting."""

@@ -28,15 +28,17 @@ plan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dt).specialize()
 Q0 = torch.zeros((8, N), dtype=dt, device=dev)
 kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2)
 for rep in range(3):
-    Q1 = torch.empty_like(Q0)
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-    e[0].record()
-    _, it1, _ = plan.ik_dls(tg, Q1, Q0=Q0, **kw)
-    e[1].record()
-    Q2, it2, err = plan.ik_coll(sdf, tg, Q1, margin=0.02, **{k: v for k, v in kw.items()})
-    e[2].record()
-    torch.cuda.synchronize()
-    print(f"N={N} stage1 {e[0].elapsed_time(e[1]) * 1e3:.1f} us  stage2 {e[1].elapsed_time(e[2]) * 1e3:.1f} us", flush=True)
+    for lanes in (1, 0):  # stage 2: attempts in sequence on one lane / side by side (auto: 4 lanes)
+        Q1 = torch.empty_like(Q0)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        _, it1, _ = plan.ik_dls(tg, Q1, Q0=Q0, **kw)
+        e[1].record()
+        Q2, it2, err = plan.ik_coll(sdf, tg, Q1, margin=0.02, lanes=lanes, **kw)
+        e[2].record()
+        torch.cuda.synchronize()
+        print(f"N={N} stage1 {e[0].elapsed_time(e[1]) * 1e3:.1f} us  stage2 (lanes={lanes}) "
+              f"{e[1].elapsed_time(e[2]) * 1e3:.1f} us", flush=True)
 for name, it in (("stage1", it1), ("stage2", it2)):
     h = np.bincount(np.minimum(it.cpu().numpy(), 129), minlength=130)
     nz = {i: int(v) for i, v in enumerate(h) if v}

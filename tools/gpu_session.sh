@@ -17,6 +17,8 @@
 #   ik-timeline                 per-lane entry / write timeline of one solve (A/B build)
 #   ik-dump                     the specialised IK source (A/B build, KINHIP_JIT_DUMP) + a kernel trace of config 4
 #   coll                        the plain-row padding A/B of the config-5 legs (tools/coll_pad_ab.py)
+#   cik                         the f3 bistage IK leg split by stage, stage 2 on one lane vs 4 (tools/cik_bench.py)
+#   coll-dump                   the specialised collision source (A/B build, KINHIP_JIT_DUMP) for offline ISA
 #   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
 set -u -o pipefail
 mkdir -p gpurun_out/prof
@@ -93,6 +95,12 @@ for step in "$@"; do
         > gpurun_out/ikprof/run.log 2>&1 || exit 7 ;;
     coll)
       timeout -k 10 200 python -u tools/coll_pad_ab.py 2>&1 | quiet || exit 8 ;;
+    cik)
+      timeout -k 10 200 python -u tools/cik_bench.py 2>&1 | quiet || exit 8 ;;
+    coll-dump)
+      mkdir -p gpurun_out/jit
+      timeout -k 10 200 env KINHIP_LIB=$AB KINHIP_JIT_DUMP=$PWD/gpurun_out/jit/coll AB_SPEC=1 \
+        python -u tools/coll_spec_ab.py 2>&1 | quiet || exit 8 ;;
     ab=*)
       spec=${step#ab=}; w=${spec%%:*}; IFS=';' read -ra sets <<< "${spec#*:}"
       timeout -k 10 900 python -u tools/ab.py $w "${sets[@]}" 2>&1 | quiet || exit 8 ;;
