@@ -339,7 +339,7 @@ def _scene_and_coll_ik_legs(ctx, stream, n, steps, spec=1):
                                    "avg_launch_us": dev_s / steps * 1e6, "algorithmic_bytes_per_sample": nbytes,
                                    "achieved_GBs": nbytes * n / (dev_s / steps) / 1e9,
                                    "valid_fraction": float((r[2] > 0).float().mean()),
-                                   "kernel": "kinhip_jit_colls_1 (specialised)" if spec else "k_coll_scene"}}
+                                   "kernel": "kinhip_jit_colls_1_2 (specialised, 2 scene groups)" if spec else "k_coll_scene"}}
     gl = m.find_link("gripper_link")
     nt = 4096
     rng = np.random.default_rng(17 + ctx.rank)

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void k_coll_scene(const KProg<T> P, const KSte
                                                     int64_t ldg, T* __restrict__ min_dist, const Tiling tl,
                                                     const SceneArgs<T> sa) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    coll_body<T, MAXA, GRAD, true>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem, sa);
+    coll_body<T, MAXA, GRAD, kMaxSceneGroups>(P, S, sph, boxes, a, q, ldq, n, dists, ldd, grads, ldg, min_dist, tl, smem, sa);
 }
 
 }  // namespace
@@ -55,13 +55,16 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
         T* dc = dists ? dists + s0 : dists;
         T* gc = grads ? grads + s0 : grads;
         T* mc = min_dist ? min_dist + s0 : min_dist;
-        if (jf && jf->coll_scene[grads ? 1 : 0]) {  // plan-specialised (kin_plan_specialize, KIN_SPEC_COLL)
+        // plan-specialised (kin_plan_specialize, KIN_SPEC_COLL): the 2-group kernel when the scene has at
+        // most 2 moving groups (24 fewer registers for the per-lane group frames than the 4-group one)
+        const hipFunction_t jk = jf ? jf->coll_scene[grads ? 1 : 0][sl.ng <= 2 ? 0 : 1] : nullptr;
+        if (jk) {
             int64_t cc = c;
             CollArgs ac = a;
             Tiling tc = tl;
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc, (void*)&ldd,
                             (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tc, (void*)&sa};
-            const hipError_t e = hipModuleLaunchKernel(jf->coll_scene[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1,
+            const hipError_t e = hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1,
                                                        (unsigned)lds, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;

@@ -179,11 +179,11 @@ struct SceneArgs {
     int32_t base_col = -1;   // scene planar base (x, y, theta) columns, -1: none
     int32_t uniform = 0;     // 1: every sample uses the scene column values of sample 0
 };
-template <typename T>
+template <typename T, int MAXG>
 struct SceneCtx {
     const KSceneGroup* groups;
     int ng;
-    T inv[kMaxSceneGroups][12];  // per lane: world -> group frame (row-major 3x4)
+    T inv[MAXG][12];  // per lane: world -> group frame (row-major 3x4); MAXG >= ng (register budget)
 };
 
 // rotation by th about the unit axis u (Rodrigues; the reference's UnitQuaternion(cos th/2, u sin th/2))
@@ -198,13 +198,13 @@ __device__ __forceinline__ void axis_rotation(const T* __restrict__ u, T th, T (
 }
 
 // the group frames of this sample (get_transform(scene, link) up to the group's moving frame), inverted
-template <typename T>
-__device__ __forceinline__ void scene_frames(SceneCtx<T>& sc, const SceneArgs<T>& sa, uint32_t off) {
+template <typename T, int MAXG>
+__device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG>& sc, const SceneArgs<T>& sa, uint32_t off) {
     sc.groups = sa.groups;
     sc.ng = sa.ng;
     const uint32_t so = sa.uniform ? 0u : off;
 #pragma unroll
-    for (int g = 0; g < kMaxSceneGroups; ++g) {
+    for (int g = 0; g < MAXG; ++g) {
         if (g >= sa.ng) break;  // uniform
         const KSceneGroup& G = sa.groups[g];
         Fr<T> f;
@@ -246,8 +246,8 @@ __device__ __forceinline__ void scene_frames(SceneCtx<T>& sc, const SceneArgs<T>
 
 // UnionSDF over the scene's groups: each group's boxes in its own frame (union_sdf), the first minimum
 // over groups; the gradient rotated back to the world
-template <typename T, bool GRAD, int NS>
-__device__ __forceinline__ void scene_union(const SceneCtx<T>& sc, const KBox<T>* __restrict__ boxes,
+template <typename T, bool GRAD, int NS, int MAXG>
+__device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const KBox<T>* __restrict__ boxes,
                                             const KAabb<T>* __restrict__ aabb, const T (&px)[NS], const T (&py)[NS],
                                             const T (&pz)[NS], T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem,
                                             bool use_lds) {
@@ -257,7 +257,7 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T>& sc, const KBox<T>
         gw[i][0] = gw[i][1] = gw[i][2] = T(0);
     }
 #pragma unroll
-    for (int g = 0; g < kMaxSceneGroups; ++g) {
+    for (int g = 0; g < MAXG; ++g) {
         if (g >= sc.ng) break;  // uniform
         const KSceneGroup& G = sc.groups[g];
         const T* I = sc.inv[g];
@@ -301,7 +301,9 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T>& sc, const KBox<T>
 #define KINHIP_JIT 0
 #endif
 
-template <typename T, int MAXA, bool GRAD, bool SCENE = false>
+// SCENE: 0 = a static union; else the union is attached to a scene with at most SCENE moving groups
+// (the per-lane group frames take 12 registers per group, so kernels come for 2 and kMaxSceneGroups)
+template <typename T, int MAXA, bool GRAD, int SCENE = 0>
 __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const Fr<T>& f, const KProg<T>& P,
                                              const KStep<T>* __restrict__ S, const KSphere<T>* __restrict__ sph,
                                              const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb,
@@ -310,7 +312,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
                                              T* __restrict__ grads, int64_t ldg, T& dmin,
                                              const unsigned char* smem, bool use_lds,
-                                             const SceneCtx<T>* sc = nullptr) {
+                                             const SceneCtx<T, SCENE ? SCENE : 1>* sc = nullptr) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
     // paired stores (KINHIP_COLL_STPAIR): every lane of the wave active, rows 8-byte aligned
     const bool pair_ok = GRAD && KINHIP_COLL_STPAIR && grads && (ldg & 1) == 0 &&
@@ -445,7 +447,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         // skip only when both spheres are beyond the truncation wave-wide (the exact path gives the
         // same results for one that is)
         const bool far = all_far(sph[k], px[0], py[0], pz[0]) && all_far(sph[k + 1], px[1], py[1], pz[1]);
-        if constexpr (SCENE) scene_union<T, GRAD, 2>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
+        if constexpr (SCENE != 0) scene_union<T, GRAD, 2, SCENE>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
         else if (!far) union_sdf<T, GRAD, 2>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
         finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
         finish(sph[k + 1], px[1], py[1], pz[1], far, ds[1], g[1]);
@@ -454,13 +456,13 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
         T px[1], py[1], pz[1], ds[1] = {T(0)}, g[1][3] = {{T(0), T(0), T(0)}};
         centre(sph[k], px[0], py[0], pz[0]);
         const bool far = all_far(sph[k], px[0], py[0], pz[0]);
-        if constexpr (SCENE) scene_union<T, GRAD, 1>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
+        if constexpr (SCENE != 0) scene_union<T, GRAD, 1, SCENE>(*sc, boxes, aabb, px, py, pz, ds, g, smem, use_lds);
         else if (!far) union_sdf<T, GRAD, 1>(boxes, aabb, na, nb, px, py, pz, ds, g, smem, use_lds);
         finish(sph[k], px[0], py[0], pz[0], far, ds[0], g[0]);
     }
 }
 
-template <typename T, int MAXA, bool GRAD, bool SCENE = false>
+template <typename T, int MAXA, bool GRAD, int SCENE = 0>
 __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __restrict__ S,
                                           const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                           const CollArgs& a, const T* __restrict__ q, int64_t ldq, int64_t n,
@@ -504,9 +506,9 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     else set_identity(f);
     const T trunc = (T)a.truncation;
     const T offs = (T)a.offset;
-    const bool broad = !SCENE && isfinite(a.truncation);  // uniform (attached boxes: no union bound)
-    SceneCtx<T> sc;
-    if constexpr (SCENE) scene_frames(sc, sa, off);  // (plain SoA only: kin_coll_batch_scene)
+    const bool broad = SCENE == 0 && isfinite(a.truncation);  // uniform (attached boxes: no union bound)
+    SceneCtx<T, SCENE ? SCENE : 1> sc;
+    if constexpr (SCENE != 0) scene_frames(sc, sa, off);  // (plain SoA only: kin_coll_batch_scene)
     const T bnd[6] = {(T)a.bc[0], (T)a.bc[1], (T)a.bc[2], (T)a.bh[0], (T)a.bh[1], (T)a.bh[2]};
     T dmin = T(INFINITY);
     T ro[MAXA][3], rz[MAXA][3];

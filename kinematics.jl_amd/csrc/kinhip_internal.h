@@ -54,7 +54,7 @@ struct JitFns {
     hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
-    hipFunction_t coll_scene[2] = {};  // the same over a union attached to a scene (kin_coll_batch_scene)
+    hipFunction_t coll_scene[2][2] = {};  // the same over an attached union [with gradients][up to 2 | 4 groups]
     hipFunction_t ikc[2][2] = {};  // collision-aware IK [rows == 6][kIkcLanes lanes per target]
 };
 
