@@ -14,7 +14,7 @@ import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
 BASE = ["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "fk6_64t", "ik32", "ik64", "coll32", "collg32", "collg32t",
-        "coll64"]
+        "coll64", "scene32", "cik32"]
 ap.add_argument("--what", default="fkjac32", choices=BASE + [w + "s" for w in BASE],
                 help="workload; a trailing 's' runs the plan-specialised kernels (kin_plan_specialize)")
 ap.add_argument("--steps", type=int, default=20)
@@ -72,6 +72,42 @@ elif a.what.startswith("fk6_64"):
         P = torch.empty((6, 12, a.n), dtype=dt, device=dev)
         for _ in range(a.steps):
             plan.run(Q, P)
+elif a.what == "scene32":  # bench f2_scene_door_sweep: boxes attached to the fridge, one door angle per sample
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    cp = sscc.plan(arm, dtype=dt)
+    if SPEC:
+        cp.specialize()
+    g = torch.Generator().manual_seed(90)
+    SQ = torch.zeros((4, a.n), dtype=torch.float64)
+    SQ[0] = torch.rand(a.n, generator=g, dtype=torch.float64) * 2.4
+    SQ[1] = 1.2
+    SQ = SQ.to(dt).to(dev).contiguous()
+    for _ in range(a.steps):
+        cp.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ)
+elif a.what == "cik32":  # bench f3_collision_ik: stage 2 (kin_ik_coll_batch) of 4,096 fridge targets
+    import numpy as np
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    sdf = kinhip.fridge_sdf(fr)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    nt = 4096
+    rng = np.random.default_rng(17)
+    tg = np.zeros((12, nt))
+    for k in range(nt):
+        x, y, z, yaw = rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32), rng.uniform(-0.3, 0.3)
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        tg[:, k] = np.concatenate([np.array([[c, -s_, 0.0], [s_, c, 0.0], [0.0, 0.0, 1.0]]).T.reshape(-1), [x, y, z]])
+    tg = torch.tensor(tg, dtype=dt, device=dev).contiguous()
+    cplan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dt)
+    if SPEC:
+        cplan.specialize()
+    Q0 = torch.zeros((8, nt), dtype=dt, device=dev)
+    Q1 = torch.empty_like(Q0)
+    kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2)
+    cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
+    for _ in range(a.steps):
+        cplan.ik_coll(sdf, tg, torch.empty_like(Q1), Q0=Q1, margin=0.02, **kw)
 elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge scene
     fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
     sdf = kinhip.fridge_sdf(fr)
