@@ -562,3 +562,60 @@ def test_gpu_attached_scene_door_sweep(dtype):
     with pytest.raises(kinhip.KinError):
         kinhip._lib.check(kinhip._lib.lib().kin_coll_batch(plan._h, sdf._h, 1.0, Q.data_ptr(), Q.stride(0), N, None, N,
                                                            None, N, M1.data_ptr(), None))
+
+
+_FOUR_GROUP_SCENE = """<?xml version="1.0"?>
+<robot name="four_groups">
+  <link name="base"><collision><origin xyz="0 0 0.5"/><geometry><box size="0.3 0.6 1.0"/></geometry></collision></link>
+  <joint name="j1" type="revolute"><parent link="base"/><child link="l1"/><origin xyz="0 0 1.0"/>
+    <axis xyz="0 0 1"/><limit lower="-3" upper="3" effort="1" velocity="1"/></joint>
+  <link name="l1"><collision><origin xyz="-0.1 0 0.1"/><geometry><box size="0.4 0.2 0.2"/></geometry></collision></link>
+  <joint name="j2" type="revolute"><parent link="l1"/><child link="l2"/><origin xyz="-0.2 0 0.2" rpy="0.3 0 0"/>
+    <axis xyz="0 1 0"/><limit lower="-2" upper="2" effort="1" velocity="1"/></joint>
+  <link name="l2"><collision><origin xyz="0 0 0.15" rpy="0 0 0.7"/><geometry><box size="0.1 0.3 0.3"/></geometry></collision></link>
+  <joint name="j3" type="prismatic"><parent link="l2"/><child link="l3"/><origin xyz="0 0 0.3"/>
+    <axis xyz="1 0 0"/><limit lower="-0.3" upper="0.3" effort="1" velocity="1"/></joint>
+  <link name="l3"><collision><origin xyz="0 0.1 0"/><geometry><box size="0.2 0.2 0.1"/></geometry></collision></link>
+</robot>
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gpu_attached_scene_four_groups_specialized_equals_generic(dtype, tmp_path):
+    """A scene whose boxes ride on four moving frames (the base and the children of three per-sample
+    scene joints, revolute and prismatic): the specialised 4-group kernels (kinhip_jit_colls_<g>_4)
+    equal the generic k_coll_scene bit for bit, and both match the oracle's static union built at a
+    sample's scene state."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(False)
+    path = tmp_path / "four_groups.urdf"
+    path.write_text(_FOUR_GROUP_SCENE)
+    sc = kinhip.parse_urdf(str(path), with_base=True)
+    js = [sc.find_joint(n) for n in ("j1", "j2", "j3")]
+    sdf = kinhip.AttachedUnionSDF(sc, js)
+    assert sdf.n_scene_cols == 6
+    N = 2000
+    g = torch.Generator().manual_seed(31)
+    Q = (torch.rand((8, N), generator=g, dtype=torch.float64) * 2.4 - 1.2).to(dtype).to(dev)
+    SQ = torch.stack([torch.rand(N, generator=g, dtype=torch.float64) * 6 - 3,
+                      torch.rand(N, generator=g, dtype=torch.float64) * 4 - 2,
+                      torch.rand(N, generator=g, dtype=torch.float64) * 0.6 - 0.3,
+                      0.6 + 0.3 * torch.rand(N, generator=g, dtype=torch.float64),
+                      0.2 * torch.rand(N, generator=g, dtype=torch.float64) - 0.1,
+                      torch.rand(N, generator=g, dtype=torch.float64) * 0.6 - 0.3]).to(dtype).to(dev).contiguous()
+    gen = sscc.plan(arm, dtype=dtype)
+    spe = sscc.plan(arm, dtype=dtype).specialize()
+    for sq in (SQ, SQ[:, 5].contiguous()):
+        for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True)):
+            for x, y in zip(gen.run(sdf, Q, scene_q=sq, **kw), spe.run(sdf, Q, scene_q=sq, **kw)):
+                assert (x is None and y is None) or torch.equal(x, y), kw
+    # one sample's state against the static union of that state (the oracle's UnionSDF there)
+    k = 11
+    st = SQ[:, k].double().cpu().numpy()
+    sc.set_joint_angles(js, st)
+    one = sscc.plan(arm, dtype=dtype).run(kinhip.UnionSDF(sc), Q[:, k:k + 1].contiguous(), dists=True)[0]
+    got = spe.run(sdf, Q, scene_q=SQ, dists=True)[0][:, k:k + 1]
+    tol = 1e-9 if dtype == torch.float64 else 1e-5
+    np.testing.assert_allclose(got.double().cpu().numpy(), one.double().cpu().numpy(), atol=tol)
