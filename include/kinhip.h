@@ -264,11 +264,10 @@ typedef struct kin_ik_params {
                            round hands attempt 0 over after 5/8 of its iterations and phase 2 resumes it
                            beside the others, bit for bit).  The two-phase scratch (first call:
                            hipMalloc of 8 sets of ~16 MiB, 64 hand-over rings each, synchronising) is
-                           per plan, with 4 sets used in
-                           turn: calls on one stream are always safe; at most 4 calls of one plan may run
-                           concurrently on different streams (a captured graph keeps the set of its
-                           captured call).  Beyond that, pass lanes > 0 (one phase) or use one plan per
-                           stream. */
+                           per plan: an eager call takes the set its stream used last, else a set whose
+                           last call has finished on the device; when 4 calls of the plan are in flight on
+                           other streams, the call runs the one-phase schedule (same results, slower)
+                           instead of sharing a set.  A captured graph keeps the set of its captured call. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */
@@ -368,10 +367,13 @@ KINHIP_API int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, doubl
 /* use_bistage) (src/inverse_kinematics.jl:1-21), many targets per launch       */
 /* ------------------------------------------------------------------------- */
 /* An IK plan of `link_id` over the q joints (kin_ik_dls_batch works on it: stage 1 of the bistage
- * solve) whose swept spheres are staged on the same chain (kin_coll_batch works on it too).  Every
- * sphere must hang, through fixed or non-batched joints, off the root -> link path; chains of at most
- * 8 steps (KIN_E_UNSUPPORTED otherwise).  Zero spheres is the plain pose problem (the reference's own
- * PR2 test builds its checker with none, test/test_inverse_kinematics.jl:63). */
+ * solve) with the tree of the target link and every swept sphere staged for kin_ik_coll_batch.  Spheres
+ * may hang off any chain of the tree (both arms of a two-arm robot, torso / head links: the reference's
+ * fridge_demo.jl scene); the solver's variables are the q joints that move the target link or a sphere
+ * (+ the planar base), the other q columns are passed through.  Limits (KIN_E_UNSUPPORTED beyond):
+ * q columns + 3 base columns <= 12, <= 32 moving joints on the needed tree, <= 64 spheres, at most 2 branch
+ * frames live at once.  Zero spheres is the plain pose problem (the reference's own PR2 test builds its
+ * checker with none, test/test_inverse_kinematics.jl:63). */
 KINHIP_API int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* desc, int32_t link_id, kin_plan** out);
 
 typedef struct kin_ik_coll_params {
@@ -385,17 +387,30 @@ typedef struct kin_ik_coll_params {
 /* Stage 2 of the bistage solve for N targets (stage 1 = kin_ik_dls_batch_from on the same plan): from
  * q0 ([n_q(+3)][ldq], read; q0 == q is in place) damped Gauss-Newton steps on the pose residual of
  * kin_ik_params.with_rot (2 = the reference's rpy objective) plus one-sided penalty rows
- * a_k = grad sdf^T J_k of the spheres inside the band, normal equations over the q joints (+ base),
- * joint limits by an active set and a clamp; restarts as in kin_ik_dls_batch (lambda > 0).  lanes: 0 = auto
- * (4 lanes per target running the attempts side by side for batches of at most 65,536 targets with
- * restarts, else 1), 1 = one lane per target (attempts in sequence), 2 / 4 / 8 = the 4-lane form;
- * identical results for every setting.
+ * a_k = grad sdf^T J_k of the spheres inside the band, normal equations over the free variables,
+ * joint limits by an active set and a clamp; restarts as in kin_ik_dls_batch (lambda > 0; every free
+ * joint re-drawn).  lanes: 0 = auto (specialised plans: a target's restart attempts side by side in 4
+ * lane groups for batches of at most 65,536 targets, its spheres shared out over 16 lanes per group
+ * while the batch has at most ~4,096 targets), 1 = one lane per target (attempts in sequence),
+ * 2 / 4 / 8 = attempts side by side on one lane each, 16 = spheres over 16 lanes, 64 = both (16 x 4);
+ * identical results for every setting (the generic kernel runs one lane whatever lanes says).
  * Converged (iters <= max_iters, else max_iters + 1) when |dp| < tol_pos, |rot| < tol_rot and every
- * sphere has d >= margin - feas.  err: [3][lde] |dp|, |rot err|, min sphere distance (or NULL). */
+ * sphere has d >= margin - feas; a target no attempt solves gets the attempt whose end state has the
+ * lowest |dp|^2 + |rot|^2 + weight^2 max(0, margin - min d)^2 (NLopt returns its best point likewise).
+ * err: [3][lde] |dp|, |rot err|, min sphere distance of the returned state (or NULL). */
 KINHIP_API int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
                                  const kin_ik_coll_params* cprm, const void* target, int64_t ldt, const void* q0,
                                  void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,
                                  void* stream);
+/* kin_ik_coll_batch against boxes attached to a scene mechanism (kin_sdf_create_attached; UnionSDF(fridge)
+ * of fridge_demo.jl / test/test_inverse_kinematics.jl:52-86): scene_q [n_scene_cols][lds] holds the scene
+ * joint values (+ base x, y, theta) of each target -- one launch solves e.g. a reach into the fridge at a
+ * different door angle per target -- or, with lds = 0, one set for the whole launch.  The scene stays
+ * fixed during a target's solve.  Runs the generic kernel (one lane per target). */
+KINHIP_API int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
+                                       const kin_ik_coll_params* cprm, const void* target, int64_t ldt,
+                                       const void* scene_q, int64_t lds, const void* q0, void* q, int64_t ldq,
+                                       int64_t n, int32_t* iters, void* err, int64_t lde, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Planning constraints over waypoints (src/planning.jl) */

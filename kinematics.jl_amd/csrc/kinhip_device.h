@@ -61,8 +61,16 @@ struct Fr {
 // reduction by pi/2 with FMA-split constants, minimax kernels on [-pi/4, pi/4]
 // (Cephes sinf/cosf for fp32, fdlibm __kernel_sin/__kernel_cos for fp64), and
 // the library call kept only behind a rarely taken |x| bound.
+#ifndef KINHIP_NOCALL_TRIG
+#define KINHIP_NOCALL_TRIG 0  // 1 (A/B fault probe only): no out-of-line call; |x| beyond the bound -> NaN
+#endif
+#if KINHIP_NOCALL_TRIG
+__device__ __forceinline__ void sincos_slow(float x, float* s, float* c) { *s = *c = __builtin_nanf(""); }
+__device__ __forceinline__ void sincos_slow(double x, double* s, double* c) { *s = *c = __builtin_nan(""); }
+#else
 __device__ __noinline__ void sincos_slow(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ __noinline__ void sincos_slow(double x, double* s, double* c) { sincos(x, s, c); }
+#endif
 
 __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
     if (__builtin_expect(!(fabsf(x) < 8192.0f), 0)) {

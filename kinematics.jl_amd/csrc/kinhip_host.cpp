@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -208,19 +209,35 @@ struct kin_plan {
     JitKernels* jit = nullptr;
     uint32_t jit_mask = 0;
     // two-phase IK schedule scratch (launch_ik_dls): allocated by the first kin_ik_dls_batch call that
-    // runs the two-phase schedule.  Eager calls use sets 0..kIkEagerSets-1 in turn (launches of one
-    // plan on several streams at once do not share a list, up to kIkEagerSets in flight); a call
-    // made inside a stream capture takes one of the remaining sets for good (the captured graph
-    // replays with it, so it never meets an eager call or another graph), and once those are gone
-    // further captures run the one-phase schedule (same results, no scratch).
+    // runs the two-phase schedule.  An eager call takes an eager set (0..kIkEagerSets-1) that is safe
+    // for its stream: the set its stream used last (stream order serialises the two calls), else one
+    // whose last call has finished on the device (ik_ev) and that no other host thread is launching
+    // into (ik_busy); when every set is in flight on other streams the call runs the one-phase
+    // schedule (same results, no scratch) instead of sharing a list.  A call made inside a stream
+    // capture takes one of the remaining sets for good (the captured graph replays with it, so it
+    // never meets an eager call or another graph), and once those are gone further captures run the
+    // one-phase schedule.
     static constexpr int kIkScratchSets = 8;
     static constexpr int kIkEagerSets = 4;
     static constexpr int64_t kIkScratchCap = int64_t(1) << 20;
     mutable std::mutex ik_mu;
     mutable void* d_ikscr = nullptr;
-    mutable std::atomic<uint32_t> ik_seq{0};
     mutable int ik_captured = 0;  // sets kIkEagerSets .. kIkEagerSets + ik_captured - 1 belong to graphs
+    mutable hipEvent_t ik_ev[kIkEagerSets] = {};      // recorded after a set's last call (null: unused)
+    mutable void* ik_stream[kIkEagerSets] = {};       // stream of that call
+    mutable bool ik_busy[kIkEagerSets] = {};          // a host thread is launching into the set
+    mutable uint32_t ik_one_phase_fallbacks = 0;      // calls that found every set in flight (tests)
+    // collision-aware IK program (kin_coll_ik_plan_create, k_ik_tree): the needed tree, host copies
+    // (plan specialisation) and one device allocation [KIkcStep<T> steps | KSphere<T> spheres]
+    KIkcProg<float> ikf{};
+    KIkcProg<double> ikd{};
+    std::vector<unsigned char> h_ikc_steps, h_ikc_sph;
+    void* d_ikc = nullptr;
+    size_t ikc_sph_off = 0;
     ~kin_plan() {
+        if (d_ikc) (void)hipFree(d_ikc);
+        for (hipEvent_t e : ik_ev)
+            if (e) (void)hipEventDestroy(e);
         if (d_ikscr) (void)hipFree(d_ikscr);
         jit_destroy(jit);
         if (d_steps) (void)hipFree(d_steps);
@@ -1058,11 +1075,14 @@ int specialize_one(kin_plan* p, uint32_t kernels) {
     if ((p->jit_mask & kernels) == kernels) return KIN_OK;
     kernels |= p->jit_mask;
     JitKernels* k = nullptr;
+    const bool ikc = p->is_coll_ik;
     const int rc = p->dtype == KIN_F32
                        ? jit_build<float>(p->pf, (const KStep<float>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
-                                          p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, kernels, &k)
+                                          p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, ikc ? &p->ikf : nullptr,
+                                          p->h_ikc_steps.data(), p->h_ikc_sph.data(), kernels, &k)
                        : jit_build<double>(p->pd, (const KStep<double>*)p->h_steps.data(), p->n_steps, p->geom.maxA,
-                                           p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, kernels, &k);
+                                           p->h_sph.empty() ? nullptr : p->h_sph.data(), p->n_sph, ikc ? &p->ikd : nullptr,
+                                           p->h_ikc_steps.data(), p->h_ikc_sph.data(), kernels, &k);
     if (rc != KIN_OK) return rc;
     jit_destroy(p->jit);
     p->jit = k;
@@ -1076,7 +1096,7 @@ int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
     if (const int rc = check_device(p->device, "kin_plan_specialize", "the plan")) return rc;
     uint32_t applies = 0;
     if (p->is_coll_ik) {
-        applies = KIN_SPEC_COLL | KIN_SPEC_IK | KIN_SPEC_IK_COLL;
+        applies = KIN_SPEC_IK | KIN_SPEC_IK_COLL;
     } else if (p->is_coll) {
         applies = KIN_SPEC_COLL;
     } else {
@@ -1444,65 +1464,316 @@ int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* c, kin_plan** 
     return KIN_OK;
 }
 
+namespace {
+// The collision-aware IK program (kinhip_prog.h KIkcProg / KIkcStep): every moving joint above the target
+// link or above a sphere link, depth first in joint order; static chains folded on the host in fp64 as
+// joint_transform does (src/mechanism.jl:90-103), frames canonical (joint axis on local z, as the Stager).
+struct IkcStepD {
+    M34 F;
+    double scale = 1;
+    int32_t kind = MOT_NONE, flags = 0, var = -1, parent_step = -1, save = -1, sph0 = 0, sph1 = 0;
+    uint32_t anc = 0;
+};
+struct IkcSphD {
+    int32_t step;  // carrier step (-1: root frame)
+    double c[3], r;
+    int32_t out;
+};
+
+int stage_ikc_tree(const kin_model& m, const kin_coll_desc* c, int32_t link_id, kin_plan& P) {
+    const int32_t L = m.n_links, J = m.n_joints();
+    const int32_t tl = link_id - 1;
+    if (tl < 0 || tl >= L) return set_error(KIN_E_KEY, "kin_coll_ik_plan_create: link id out of range");
+    const int32_t nq = c->n_q, base_col = m.with_base ? nq : -1;
+    const int32_t nv = nq + (m.with_base ? 3 : 0);
+    if (nv > kIkcMaxVars)
+        return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: " + std::to_string(nv) + " variables (q columns + base; max " +
+                                                std::to_string(kIkcMaxVars) + ")");
+    if (c->n_spheres > kIkcMaxSpheres)
+        return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: more than " + std::to_string(kIkcMaxSpheres) + " spheres");
+    std::vector<int32_t> qcol(J, -1);
+    for (int32_t k = 0; k < nq; ++k) {
+        const int32_t j = c->q_joint_ids[k] - 1;
+        if (j < 0 || j >= J) return set_error(KIN_E_KEY, "kin_coll_ik_plan_create: q joint id out of range");
+        qcol[j] = k;  // set_joint_angles: a repeated joint keeps the last column
+    }
+    std::vector<char> needed(L, 0);
+    auto mark = [&](int32_t l) {
+        for (int32_t x = l; x >= 0 && !needed[x]; x = m.plink(x)) needed[x] = 1;
+    };
+    mark(tl);
+    std::vector<std::vector<int32_t>> sph_of(L);
+    for (int32_t k = 0; k < c->n_spheres; ++k) {
+        const int32_t lk = c->sphere_link_ids[k] - 1;
+        if (lk < 0 || lk >= L) return set_error(KIN_E_KEY, "kin_coll_ik_plan_create: sphere link id out of range");
+        mark(lk);
+        sph_of[lk].push_back(k);
+    }
+    const uint32_t base_bits = m.with_base ? (7u << base_col) : 0u;
+    std::vector<IkcStepD> steps;
+    std::vector<IkcSphD> spheres;
+    int32_t tgt_step = kIkcRoot;
+    M34 Xt = m_identity();
+    uint32_t prism = 0, joints = 0;
+    // depth first from every root: `carrier` = step whose post-motion canonical frame carries link x,
+    // S = that frame -> link x (static)
+    std::function<int(int32_t, int32_t, const M34&, uint32_t)> visit = [&](int32_t x, int32_t carrier, const M34& S,
+                                                                            uint32_t anc) -> int {
+        if (x == tl) {
+            tgt_step = carrier < 0 ? kIkcRoot : carrier;
+            Xt = S;
+        }
+        for (int32_t k : sph_of[x]) {
+            IkcSphD sd;
+            const double c0 = c->centers ? c->centers[3 * k] : 0.0;
+            const double c1 = c->centers ? c->centers[3 * k + 1] : 0.0;
+            const double c2 = c->centers ? c->centers[3 * k + 2] : 0.0;
+            for (int i = 0; i < 3; ++i) sd.c[i] = S.r[3 * i] * c0 + S.r[3 * i + 1] * c1 + S.r[3 * i + 2] * c2 + S.t[i];
+            sd.r = c->radii[k];
+            sd.out = k;
+            sd.step = carrier;
+            spheres.push_back(sd);
+        }
+        for (int32_t j : m.child_joints[x]) {
+            const int32_t ch = m.jclink[j] - 1;
+            if (!needed[ch]) continue;
+            const bool moving = qcol[j] >= 0 && m.jtype[j] != KIN_JOINT_FIXED;
+            if (!moving) {  // static: folded (joint held at m.angles)
+                const int rc = visit(ch, carrier, m_mul(S, m.joint_tf(j, m.angles[j])), anc);
+                if (rc != KIN_OK) return rc;
+                continue;
+            }
+            if ((int32_t)steps.size() >= kIkcMaxSteps)
+                return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: more than " + std::to_string(kIkcMaxSteps) +
+                                                        " moving joints on the needed tree");
+            double scale;
+            const M34 A = align_z(&m.jaxis[3 * j], &scale);
+            IkcStepD st;
+            st.F = m_mul(m_mul(S, m.pose(j)), A);
+            st.scale = scale;
+            st.kind = m.jtype[j] == KIN_JOINT_PRISMATIC ? MOT_PRISM : MOT_REV;
+            if (st.kind == MOT_REV && scale != 1.0) st.flags |= SF_SCALE;
+            st.var = qcol[j];
+            st.parent_step = carrier;
+            st.anc = anc | (1u << qcol[j]);
+            joints |= 1u << qcol[j];
+            if (st.kind == MOT_PRISM) prism |= 1u << qcol[j];
+            const int32_t s = (int32_t)steps.size();
+            steps.push_back(st);
+            const int rc = visit(ch, s, m_rot_transpose(A), st.anc);
+            if (rc != KIN_OK) return rc;
+        }
+        return KIN_OK;
+    };
+    for (int32_t l = 0; l < L; ++l)
+        if (needed[l] && m.link_pjoint[l] < 0) {
+            const int rc = visit(l, -1, m_identity(), base_bits);
+            if (rc != KIN_OK) return rc;
+        }
+    // spheres in carrier order (root first, then the walk's step order), the caller's order inside a carrier
+    std::stable_sort(spheres.begin(), spheres.end(), [](const IkcSphD& a, const IkcSphD& b) { return a.step < b.step; });
+    int32_t sph_root0 = 0, sph_root1 = 0;
+    for (size_t k = 0; k < spheres.size(); ++k) {
+        const int32_t s = spheres[k].step;
+        if (s < 0) {
+            sph_root1 = (int32_t)k + 1;
+        } else {
+            if (steps[s].sph1 == 0) steps[s].sph0 = (int32_t)k;
+            steps[s].sph1 = (int32_t)k + 1;
+        }
+    }
+    // branch frames: a step whose frame a later, non-adjacent step starts from is saved into a slot, live
+    // from the step to its last such child
+    const int32_t ns = (int32_t)steps.size();
+    std::vector<int32_t> last_use(ns, -1);
+    for (int32_t s = 0; s < ns; ++s) {
+        const int32_t p = steps[s].parent_step;
+        if (p >= 0 && p != s - 1) last_use[p] = std::max(last_use[p], s);
+    }
+    std::vector<int32_t> slot_of(ns, -1), slot_free_at(kIkcMaxSlots, -1);
+    for (int32_t s = 0; s < ns; ++s) {
+        if (last_use[s] < 0) continue;
+        int sl = -1;
+        for (int k = 0; k < kIkcMaxSlots && sl < 0; ++k)
+            if (slot_free_at[k] <= s) sl = k;
+        if (sl < 0)
+            return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: the tree needs more than " +
+                                                    std::to_string(kIkcMaxSlots) + " saved branch frames");
+        slot_of[s] = sl;
+        slot_free_at[sl] = last_use[s];
+        steps[s].save = sl;
+    }
+    uint32_t tgt_mask = tgt_step == kIkcRoot ? base_bits : steps[tgt_step].anc;
+    uint32_t free_mask = tgt_mask;
+    for (const IkcSphD& sd : spheres) free_mask |= sd.step < 0 ? base_bits : steps[sd.step].anc;
+    auto fill = [&](auto& K, auto* st_out, auto* sp_out) {
+        using T = std::remove_reference_t<decltype(K.Xt[0])>;
+        K = {};
+        K.nS = ns;
+        K.nv = nv;
+        K.n_q = nq;
+        K.base_col = base_col;
+        K.n_sph = (int32_t)spheres.size();
+        K.sph_root0 = sph_root0;
+        K.sph_root1 = sph_root1;
+        K.tgt_step = tgt_step;
+        K.has_xt = !m_is_identity(Xt);
+        K.tgt_mask = tgt_mask;
+        K.free_mask = free_mask;
+        K.joint_mask = joints;
+        K.prism_mask = prism;
+        to_row12<T>(Xt, K.Xt);
+        for (int v = 0; v < kIkcMaxVars; ++v) {
+            K.vlo[v] = (T)-INFINITY;
+            K.vhi[v] = (T)INFINITY;
+        }
+        for (int32_t j = 0; j < J; ++j)
+            if (qcol[j] >= 0 && ((joints >> qcol[j]) & 1u)) {
+                K.vlo[qcol[j]] = (T)m.jlo[j];
+                K.vhi[qcol[j]] = (T)m.jhi[j];
+            }
+        for (int32_t s = 0; s < ns; ++s) {
+            const IkcStepD& a = steps[s];
+            auto& b = st_out[s];
+            memset(&b, 0, sizeof(b));
+            to_row12<T>(a.F, b.F);
+            b.scale = (T)a.scale;
+            b.kind = a.kind;
+            b.flags = a.flags;
+            b.var = a.var;
+            b.parent = a.parent_step < 0 ? kIkcRoot : a.parent_step == s - 1 ? kIkcPrev : slot_of[a.parent_step];
+            b.save = a.save;
+            b.sph0 = a.sph0;
+            b.sph1 = a.sph1;
+            b.anc = a.anc;
+        }
+        for (size_t k = 0; k < spheres.size(); ++k) {
+            auto& b = sp_out[k];
+            memset(&b, 0, sizeof(b));
+            for (int i = 0; i < 3; ++i) b.c[i] = (T)spheres[k].c[i];
+            b.r = (T)spheres[k].r;
+            b.out = spheres[k].out;
+            b.anc = spheres[k].step < 0 ? base_bits : steps[spheres[k].step].anc;
+        }
+    };
+    const bool f32 = c->dtype == KIN_F32;
+    const size_t est = f32 ? sizeof(KIkcStep<float>) : sizeof(KIkcStep<double>);
+    const size_t esp = f32 ? sizeof(KSphere<float>) : sizeof(KSphere<double>);
+    P.h_ikc_steps.assign(std::max<size_t>(1, ns) * est, 0);
+    P.h_ikc_sph.assign(std::max<size_t>(1, spheres.size()) * esp, 0);
+    if (f32)
+        fill(P.ikf, (KIkcStep<float>*)P.h_ikc_steps.data(), (KSphere<float>*)P.h_ikc_sph.data());
+    else
+        fill(P.ikd, (KIkcStep<double>*)P.h_ikc_steps.data(), (KSphere<double>*)P.h_ikc_sph.data());
+    return KIN_OK;
+}
+
+// the staged tree program to the device: [steps | spheres] in one allocation
+int upload_ikc_tree(kin_plan& P) {
+    P.ikc_sph_off = (P.h_ikc_steps.size() + 255) / 256 * 256;
+    const size_t bytes = P.ikc_sph_off + P.h_ikc_sph.size();
+    std::vector<unsigned char> host(bytes, 0);
+    memcpy(host.data(), P.h_ikc_steps.data(), P.h_ikc_steps.size());
+    memcpy(host.data() + P.ikc_sph_off, P.h_ikc_sph.data(), P.h_ikc_sph.size());
+    hipError_t e = hipMalloc(&P.d_ikc, bytes);
+    if (e != hipSuccess) {
+        P.d_ikc = nullptr;
+        return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    e = hipMemcpy(P.d_ikc, host.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("hipMemcpy: ") + hipGetErrorString(e));
+    return KIN_OK;
+}
+}  // namespace
+
 int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* c, int32_t link_id, kin_plan** out) {
     if (!m || !c || !out) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: null argument");
     if (c->n_spheres < 0 || (c->n_spheres && (!c->sphere_link_ids || !c->radii)))
         return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: spheres need link ids and radii");
     if (c->n_q < 1 || !c->q_joint_ids) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: no q joints");
     const int32_t out_ids[1] = {link_id};
-    // an IK plan of `link` over the q joints (get_jacobian! over them, geometric rows) whose spheres are
-    // staged on the same chain (every sphere must hang off the root -> link path)
+    // an IK plan of `link` over the q joints (stage 1: get_jacobian! over them, geometric rows) ...
     kin_plan_desc d{c->dtype, c->n_q, c->q_joint_ids, 1, out_ids, link_id, c->n_q, c->q_joint_ids, KIN_WITH_ROT};
     auto P = std::make_unique<kin_plan>();
+    // ... and the tree of the target link and every sphere (stage 2, k_ik_tree; staged on the host first)
+    int rc = stage_ikc_tree(*m, c, link_id, *P);
+    if (rc != KIN_OK) return rc;
     Stager st(*m, d);
-    st.coll = c;
-    const int rc = st.run(*P);
+    rc = st.run(*P);
     if (rc != KIN_OK) return rc;
     if (!P->ik_ok) return set_error(KIN_E_INVALID, "kin_coll_ik_plan_create: " + P->ik_why);
-    if (P->geom.maxA > kIkcMaxChain)
-        return set_error(KIN_E_UNSUPPORTED, "kin_coll_ik_plan_create: chains of more than " +
-                                                std::to_string(kIkcMaxChain) + " steps are not supported");
+    rc = upload_ikc_tree(*P);
+    if (rc != KIN_OK) return rc;
     P->is_coll_ik = true;
+    P->n_sph = c->n_spheres;
     *out = P.release();
     return KIN_OK;
 }
 
-int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
-                      const void* target, int64_t ldt, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters,
-                      void* err, int64_t lde, void* stream) {
-    if (!p || !sdf || !prm || !cp) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: null argument");
-    if (!p->is_coll_ik) return set_error(KIN_E_INVALID, "kin_ik_coll_batch: plan was not made by kin_coll_ik_plan_create");
-    if (sdf->attached) return set_error(KIN_E_UNSUPPORTED, "kin_ik_coll_batch: boxes attached to a scene mechanism");
-    if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
+namespace {
+int ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
+                  const void* target, int64_t ldt, const void* scene_q, int64_t lds, bool scene, const void* q0, void* q,
+                  int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream, const char* fn) {
+    auto bad = [&](int code, const std::string& w) { return set_error(code, std::string(fn) + ": " + w); };
+    if (!p || !sdf || !prm || !cp) return bad(KIN_E_INVALID, "null argument");
+    if (!p->is_coll_ik) return bad(KIN_E_INVALID, "plan was not made by kin_coll_ik_plan_create");
+    if (sdf->attached && !scene) return bad(KIN_E_INVALID, "the kin_sdf is attached to a scene: use kin_ik_coll_batch_scene");
+    if (!sdf->attached && scene) return bad(KIN_E_INVALID, "the kin_sdf is not attached to a scene (use kin_ik_coll_batch)");
+    if (n < 0) return bad(KIN_E_INVALID, "n < 0");
     if (n == 0) return KIN_OK;
-    if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return set_error(KIN_E_INVALID, "bad pointer / stride");
-    if (const int rc = check_device(p->device, "kin_ik_coll_batch", "the plan")) return rc;
-    if (const int rc = check_device(sdf->device, "kin_ik_coll_batch", "the kin_sdf")) return rc;
+    if (!target || ldt < n || !q || ldq < n || (err && lde < n)) return bad(KIN_E_INVALID, "bad pointer / stride");
+    if (scene && sdf->scene_cols > 0 && (!scene_q || (lds != 0 && lds < n))) return bad(KIN_E_INVALID, "bad scene_q / lds");
+    if (const int rc = check_device(p->device, fn, "the plan")) return rc;
+    if (const int rc = check_device(sdf->device, fn, "the kin_sdf")) return rc;
     if (prm->max_iters < 0 || !(prm->lambda > 0) || !(prm->max_step > 0) || prm->restarts < 0 ||
         prm->with_rot < 0 || prm->with_rot > 2 || prm->index_base < 0)
-        return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad IK parameters (lambda must be > 0)");
+        return bad(KIN_E_INVALID, "bad IK parameters (lambda must be > 0)");
     if (!std::isfinite(cp->margin) || !(cp->band >= 0) || !(cp->weight > 0) || !(cp->feas >= 0))
-        return set_error(KIN_E_INVALID, "kin_ik_coll_batch: bad collision parameters");
-    if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
-        return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
+        return bad(KIN_E_INVALID, "bad collision parameters");
+    if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8 &&
+        prm->lanes != 16 && prm->lanes != 64)
+        return bad(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4, 8, 16 or 64");
     const IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
                    prm->restarts, prm->seed, prm->lanes, prm->index_base};
     const IkcArgs c{cp->margin, cp->band, cp->weight, cp->feas};
     const CollArgs ca{INFINITY, 0.0, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
                       {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};
+    const bool f32 = p->dtype == KIN_F32;
+    const void* sc = f32 ? sdf->d_scene_f32 : sdf->d_scene_f64;
+    const SceneLaunch sl{sc, sc ? (const char*)sc + sdf->scene_steps_off : nullptr, scene_q, lds, sdf->n_groups,
+                         sdf->scene_base_col, lds == 0 ? 1 : 0};
+    const JitFns* jf = jit_fns(p->jit);  // (the specialised kernels take the static union only)
+    const void* st = p->d_ikc;
+    const void* sp = (const char*)p->d_ikc + p->ikc_sph_off;
     hipError_t e;
-    if (p->dtype == KIN_F32)
-        e = launch_ik_coll<float>(p->pf, (const KStep<float>*)p->d_steps, (const KSphere<float>*)p->d_sph,
-                                  (const KBox<float>*)sdf->d_f32, p->geom, ca, c, a, (const float*)target, ldt,
-                                  (const float*)(q0 == q ? nullptr : q0), (float*)q, ldq, n, iters, (float*)err, lde,
-                                  jit_fns(p->jit), (hipStream_t)stream);
+    if (f32)
+        e = launch_ik_tree<float>(p->ikf, (const KIkcStep<float>*)st, (const KSphere<float>*)sp, (const KBox<float>*)sdf->d_f32,
+                                  ca, scene ? &sl : nullptr, c, a, (const float*)target, ldt,
+                                  (const float*)(q0 == q ? nullptr : q0), (float*)q, ldq, n, iters, (float*)err, lde, jf,
+                                  (hipStream_t)stream);
     else
-        e = launch_ik_coll<double>(p->pd, (const KStep<double>*)p->d_steps, (const KSphere<double>*)p->d_sph,
-                                   (const KBox<double>*)sdf->d_f64, p->geom, ca, c, a, (const double*)target, ldt,
-                                   (const double*)(q0 == q ? nullptr : q0), (double*)q, ldq, n, iters, (double*)err,
-                                   lde, jit_fns(p->jit), (hipStream_t)stream);
-    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_coll launch: ") + hipGetErrorString(e));
+        e = launch_ik_tree<double>(p->ikd, (const KIkcStep<double>*)st, (const KSphere<double>*)sp,
+                                   (const KBox<double>*)sdf->d_f64, ca, scene ? &sl : nullptr, c, a, (const double*)target,
+                                   ldt, (const double*)(q0 == q ? nullptr : q0), (double*)q, ldq, n, iters, (double*)err,
+                                   lde, jf, (hipStream_t)stream);
+    if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_ik_tree launch: ") + hipGetErrorString(e));
     return KIN_OK;
+}
+}  // namespace
+
+int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
+                      const void* target, int64_t ldt, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters,
+                      void* err, int64_t lde, void* stream) {
+    return ik_coll_batch(p, sdf, prm, cp, target, ldt, nullptr, 0, false, q0, q, ldq, n, iters, err, lde, stream,
+                         "kin_ik_coll_batch");
+}
+
+int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
+                            const kin_ik_coll_params* cp, const void* target, int64_t ldt, const void* scene_q,
+                            int64_t lds, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* err,
+                            int64_t lde, void* stream) {
+    return ik_coll_batch(p, sdf, prm, cp, target, ldt, scene_q, lds, true, q0, q, ldq, n, iters, err, lde, stream,
+                         "kin_ik_coll_batch_scene");
 }
 
 namespace {
@@ -1702,6 +1973,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     // two-phase schedule scratch (small batches with restarts; launch_ik_dls): only a call that runs
     // that schedule touches it, so every other call stays allocation-free (capture-safe)
     IkScratch scr;
+    int eager_set = -1;  // eager scratch set taken by this call (released after the launch)
     if (ik_wants_two_phase(a, n, kin_plan::kIkScratchCap)) {
         // kIkSubRings rings of 2 * cap / kIkSubRings entries (a phase-1 launch spreads its hand-overs over
         // the rings by wave; twice the even share covers the uneven last waves), list + aux, and the
@@ -1729,12 +2001,27 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     return set_error(KIN_E_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e0));
                 }
             }
-            if (!capturing)
-                set = (int)(p->ik_seq.fetch_add(1) % kin_plan::kIkEagerSets);
-            else if (kin_plan::kIkEagerSets + p->ik_captured < kin_plan::kIkScratchSets)
+            if (!capturing) {
+                // the set this stream used last, else a finished one, else none (one phase)
+                for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
+                    if (!p->ik_busy[k] && p->ik_ev[k] && p->ik_stream[k] == stream) set = k;
+                for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
+                    if (!p->ik_busy[k] && (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess)) set = k;
+                if (set >= 0) {
+                    if (!p->ik_ev[set] && hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming) != hipSuccess) {
+                        p->ik_ev[set] = nullptr;
+                        set = -1;
+                    } else {
+                        p->ik_busy[set] = true;
+                    }
+                } else {
+                    ++p->ik_one_phase_fallbacks;
+                }
+            } else if (kin_plan::kIkEagerSets + p->ik_captured < kin_plan::kIkScratchSets)
                 set = kin_plan::kIkEagerSets + p->ik_captured++;
         }
-        if (set >= 0) {  // (no set left for a captured call: one phase)
+        if (set >= 0 && !capturing) eager_set = set;
+        if (set >= 0) {  // (no set left: one phase)
             unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * set;
             scr.fail_ctl = (uint32_t*)base;
             scr.fail_list = (int32_t*)(base + ctl_bytes);
@@ -1751,6 +2038,16 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
                                   (const double*)q0, (double*)q, ldq, n, iters, (double*)err, lde, jf, scr,
                                   (hipStream_t)stream);
+    if (eager_set >= 0) {  // the set is free again once this call has run on its stream
+        std::lock_guard<std::mutex> lk(p->ik_mu);
+        if (hipEventRecord(p->ik_ev[eager_set], (hipStream_t)stream) == hipSuccess) {
+            p->ik_stream[eager_set] = stream;
+        } else {  // (cannot tell when it finishes: a fresh event, queried as finished, would lie)
+            (void)hipStreamSynchronize((hipStream_t)stream);
+            p->ik_stream[eager_set] = stream;
+        }
+        p->ik_busy[eager_set] = false;
+    }
     if (e != hipSuccess)
         return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e) +
                                            (ik_last_call_partial() ? " (phase 2 failed to launch after phase 1: the "

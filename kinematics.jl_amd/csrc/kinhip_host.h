@@ -16,7 +16,7 @@ struct JitKernels;
 struct JitFns;
 template <typename T>
 int jit_build(const KProg<T>& P, const KStep<T>* steps, int nsteps, int maxA, const void* spheres, int n_sph,
-              uint32_t kernels, JitKernels** out);
+              const KIkcProg<T>* ikc, const void* ikc_steps, const void* ikc_sph, uint32_t kernels, JitKernels** out);
 void jit_destroy(JitKernels* k);
 const JitFns* jit_fns(const JitKernels* k);  // null for a null k
 int jit_selfcheck();

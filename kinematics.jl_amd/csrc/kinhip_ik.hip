@@ -1,7 +1,7 @@
 // kinhip_ik.hip -- k_ik_dls (batched DLS IK with restarts) and k_nakamura.
 // (gfx950 only; shared helpers in kinhip_device.h)
 #include "kinhip_ik_dev.h"
-#include "kinhip_ikc_dev.h"
+#include "kinhip_ikt_dev.h"
 
 namespace kinhip {
 namespace {
@@ -27,15 +27,18 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
     nakamura_body<T, MAXA>(P, S, pts, ldpt, q, ldq, n);
 }
 
-template <typename T, int MAXA, int ROWS, int G>
-__global__ __launch_bounds__(64) void k_ik_coll(const KProg<T> P, const KStep<T>* __restrict__ S,
+// generic collision-aware IK: one lane per target (attempts in sequence), the program from memory;
+// MAXG > 0: boxes attached to a scene, scene joint values per target
+template <typename T, int MAXV, int ROWS, int MAXG>
+__global__ __launch_bounds__(64) void k_ik_tree(const KIkcProg<T> P, const KIkcStep<T>* __restrict__ S,
                                                 const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
                                                 const CollArgs ca, const IkcArgsT<T> cz, const IkArgsT<T> a,
-                                                const T* __restrict__ tgt, int64_t ldt, T* __restrict__ q, int64_t ldq,
-                                                int64_t n, int32_t* __restrict__ iters, T* __restrict__ err,
-                                                int64_t lde) {
+                                                const SceneArgs<T> sa, const T* __restrict__ tgt, int64_t ldt,
+                                                T* __restrict__ q, int64_t ldq, int64_t n, int32_t* __restrict__ iters,
+                                                T* __restrict__ err, int64_t lde) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ikc_body<T, MAXA, ROWS, G>(P, S, sph, boxes, ca, cz, a, tgt, ldt, q, ldq, n, iters, err, lde, smem);
+    ikt_body<T, MAXV, ROWS, 1, 1, 1, MAXG>(P, S, sph, boxes, ca, cz, a, sa, tgt, ldt, q, ldq, n, iters, err, lde,
+                                                 smem);
 }
 
 }  // namespace
@@ -244,33 +247,54 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     return hipSuccess;
 }
 
-// Lanes per k_ik_coll target: 4 (attempts side by side, ikc_body) in the plan-specialised kernels while
-// the batch is small enough that the lanes would idle otherwise (<= 65,536 targets, the ik_group rule)
-// and the schedule has at least 4 attempts, else 1; kin_ik_params.lanes = 1 forces one lane, 2 / 4 / 8
-// ask for the 4-lane form.  Identical results.  The generic kernels keep one lane per target: their fp64
-// 4-lane instantiation (~500 registers, SGPR spills, an out-of-line sincos call) faulted once on the GPU
-// (illegal address, with idle fourth lanes at 3 attempts; profiles/r03_ikc_lanes.txt), cause not found.
-static int ikc_group(int64_t n, int natt, int lanes, bool spec) {
-    static const int env = ab_env_int("KINHIP_IKC_GROUP", 0);
-    const int forced = lanes ? lanes : env;
-    if (!spec || natt < kIkcLanes || forced == 1) return 1;
-    return forced > 1 || n * 8 <= (int64_t(1) << 19) ? kIkcLanes : 1;
+// Lanes of a k_ik_tree target (specialised kernels): G attempt groups run a target's restart attempts
+// side by side, S sphere lanes per group share out its spheres -- identical results for every (S, G).
+// Small batches fill the chip only this way (the bistage solve's few thousand targets are a fraction of
+// a wave per SIMD): G = 4 while there are restart attempts and up to 2^16 targets, S = 16 while the
+// whole batch stays within ~4 waves per SIMD (n * G * 16 <= 2^18 lanes), else S = 1.
+// kin_ik_params.lanes forces a form: 1 = one lane, 2 / 4 / 8 = 4 attempt groups of one lane, 16 = 16
+// sphere lanes x 1, 64 = 16 x 4; KINHIP_IKT_S / KINHIP_IKT_G override (A/B build).
+static int ikt_variant(int64_t n, int natt, int lanes) {
+    static const int s_env = ab_env_int("KINHIP_IKT_S", 0), g_env = ab_env_int("KINHIP_IKT_G", 0);
+    if (lanes == 1) return 0;
+    if (lanes == 2 || lanes == 4 || lanes == 8) return 1;
+    if (lanes == 16) return 2;
+    if (lanes == 64) return 3;
+    int G = natt >= 2 && n <= (int64_t(1) << 16) ? 4 : 1;
+    int S = n * G * 16 <= (int64_t(1) << 18) ? 16 : 1;
+    if (s_env) S = s_env;
+    if (g_env) G = g_env;
+    for (int v = 0; v < kIktVariants; ++v)
+        if (kIktS[v] == S && kIktG[v] == G) return v;
+    return 0;
 }
 
-// k_ik_coll: G lanes per target (ikc_group), 64-lane workgroups (a few thousand targets still spread
-// over many CUs); the union's boxes in LDS for the argmin gathers (k_coll)
 template <typename T>
-hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
-                          const LaunchGeom& g, const CollArgs& ca, const IkcArgs& c, const IkArgs& a, const T* target,
-                          int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err, int64_t lde,
-                          const JitFns* jf, hipStream_t st) {
+hipError_t launch_ik_tree(const KIkcProg<T>& P, const KIkcStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                          const CollArgs& ca, const SceneLaunch* scene, const IkcArgs& c, const IkArgs& a,
+                          const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
+                          T* err, int64_t lde, const JitFns* jf, hipStream_t st) {
     int L, natt;
     ik_attempts(a, &L, &natt);
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
                   0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
     const IkcArgsT<T> cz{T(c.margin), T(c.band), T(c.weight), T(c.feas)};
     const size_t lds = ca.n_boxes <= kCollLdsBoxes ? (size_t)ca.n_boxes * sizeof(KBox<T>) : 0;
-    const int G = ikc_group(n, natt, a.lanes, jf && jf->ikc[a.with_rot ? 1 : 0][1]);
+    const int rows6 = a.with_rot ? 1 : 0;
+    // the specialised kernels take a static union; a scene's union runs the generic kernel
+    const int vi = (jf && !scene) ? ikt_variant(n, natt, a.lanes) : 0;
+    const hipFunction_t jk = (jf && !scene) ? jf->ikt[rows6][vi] : nullptr;
+    const int lanes = jk ? kIktS[vi] * kIktG[vi] : 1;
+    SceneArgs<T> sa{};
+    if (scene) {
+        sa.groups = (const KSceneGroup*)scene->groups;
+        sa.steps = (const KSceneStep<T>*)scene->steps;
+        sa.q = (const T*)scene->q;
+        sa.ld = scene->ld;
+        sa.ng = scene->ng;
+        sa.base_col = scene->base_col;
+        sa.uniform = scene->uniform;
+    }
     for (int64_t s0 = 0; s0 < n; s0 += kIkChunk) {
         const int64_t cn = std::min(kIkChunk, n - s0);
         at.ibase = a.index_base + s0;
@@ -279,8 +303,9 @@ hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSpher
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
-        const unsigned grid = (unsigned)((cn * G + 63) / 64);
-        const hipFunction_t jk = jf ? jf->ikc[a.with_rot ? 1 : 0][G > 1 ? 1 : 0] : nullptr;
+        SceneArgs<T> sac = sa;
+        if (scene && !sa.uniform) sac.q = sa.q + s0;
+        const unsigned grid = (unsigned)((cn * lanes + 63) / 64);
         if (jk) {
             int64_t cc = cn;
             CollArgs cac = ca;
@@ -291,16 +316,17 @@ hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSpher
             if (e != hipSuccess) return e;
             continue;
         }
-#define KIN_IKC(MA, R) \
-        hipLaunchKernelGGL((k_ik_coll<T, MA, R, 1>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, tc, ldt, qc, ldq, cn, ic, ec, lde)
-        if (g.maxA == 4) {
-            if (a.with_rot) KIN_IKC(4, 6); else KIN_IKC(4, 3);
-        } else if (g.maxA == 8) {
-            if (a.with_rot) KIN_IKC(8, 6); else KIN_IKC(8, 3);
+#define KIN_IKT(MV, R, MG) \
+        hipLaunchKernelGGL((k_ik_tree<T, MV, R, MG>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, sac, tc, ldt, qc, ldq, cn, ic, ec, lde)
+        // (variables bound 8 or 12: the normal equations and joint records live in registers)
+        if (scene) {
+            if (a.with_rot) KIN_IKT(kIkcMaxVars, 6, kMaxSceneGroups); else KIN_IKT(kIkcMaxVars, 3, kMaxSceneGroups);
+        } else if (P.nv <= 8) {
+            if (a.with_rot) KIN_IKT(8, 6, 0); else KIN_IKT(8, 3, 0);
         } else {
-            return hipErrorNotSupported;  // (kin_coll_ik_plan_create refuses longer chains)
+            if (a.with_rot) KIN_IKT(kIkcMaxVars, 6, 0); else KIN_IKT(kIkcMaxVars, 3, 0);
         }
-#undef KIN_IKC
+#undef KIN_IKT
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -337,10 +363,10 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
                                          const JitFns*, const IkScratch&, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
                                            int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);          \
-    template hipError_t launch_ik_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, \
-                                          const LaunchGeom&, const CollArgs&, const IkcArgs&, const IkArgs&,    \
-                                          const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*,       \
-                                          int64_t, const JitFns*, hipStream_t);
+    template hipError_t launch_ik_tree<T>(const KIkcProg<T>&, const KIkcStep<T>*, const KSphere<T>*,          \
+                                          const KBox<T>*, const CollArgs&, const SceneLaunch*, const IkcArgs&,   \
+                                          const IkArgs&, const T*, int64_t, const T*, T*, int64_t, int64_t,      \
+                                          int32_t*, T*, int64_t, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

@@ -1,0 +1,603 @@
+// kinhip_ikt_dev.h -- device body of k_ik_tree: batched collision-aware IK, the second stage of
+// inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage) (src/inverse_kinematics.jl:
+// 1-21): the pose objective subject to IneqConst(sscc, joints, sdf, 1, margin) (src/planning.jl:55-68,
+// every swept sphere at least `margin` from the UnionSDF).  Included by kinhip_ik.hip (generic
+// kernels) and embedded in the run-time specialised source (kinhip_jit.cpp).  gfx950 only.
+//
+// The program (KIkcProg / KIkcStep, kinhip_prog.h) is the needed kinematic tree: spheres may hang off
+// any moving chain (both arms of a two-arm robot, head / torso links), the target link off another;
+// the variables are the q columns (+ the planar base), each moved by one joint of the tree.  The
+// boxes may be a static UnionSDF or one attached to a scene mechanism (kin_sdf_create_attached) whose
+// joint values are given per target (a door angle per target: fridge_demo.jl).
+#pragma once
+#include "kinhip_coll_dev.h"
+#include "kinhip_ik_dev.h"
+
+// Contraction only inside one expression (a * b + c): the specialised kernels fold constants into the
+// instruction stream, and fusing across statements would then differ from the generic kernels
+#pragma clang fp contract(on)
+
+// the specialised kernels unroll the tree walk and the sphere loops (constant trip counts)
+#ifdef KINHIP_JIT
+#define KIN_IKT_UNROLL _Pragma("unroll")
+#else
+#define KIN_IKT_UNROLL
+#endif
+
+namespace kinhip {
+namespace {
+
+// Constraint handling of the collision-aware IK (kin_ik_coll_params)
+template <typename T>
+struct IkcArgsT {
+    T margin;  // IneqConst margin (the reference's stage 2 uses 0.02)
+    T band;    // a sphere with d < margin + band is pushed towards margin + band
+    T weight;  // weight of a sphere's row against the pose rows
+    T feas;    // converged only when every sphere has d >= margin - feas
+};
+
+// a[i] for a uniform (generic kernel) or constant (specialised kernel) index: selects, never a
+// dynamically indexed register array (which the compiler would move to scratch memory)
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&a)[N], int i) {
+    T v = a[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) v = (i == k) ? a[k] : v;
+    return v;
+}
+template <typename T, int N>
+__device__ __forceinline__ void put(T (&a)[N], int i, T v) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) a[k] = (i == k) ? v : a[k];
+}
+template <typename T, int N>
+__device__ __forceinline__ void pick_frame(Fr<T>& f, const Fr<T> (&a)[N], int i) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (i == k) f = a[k];
+}
+template <typename T, int N>
+__device__ __forceinline__ void put_frame(Fr<T> (&a)[N], int i, const Fr<T>& f) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        if (i == k) a[k] = f;
+}
+
+// The IneqConst row of one sphere (k_coll's gradient, src/collision.jl:67-94): a_v = g . d(c)/d(q_v) for
+// the variables moving the sphere's frame (anc), 0 elsewhere.  Joints: revolute z_v . (c x g) - g . m_v
+// (m = z x o, the record), prismatic g . z_v; base [g0, g1, -g0 (c_y - b_y) + g1 (c_x - b_x)].
+template <typename T, int MAXV>
+__device__ __forceinline__ void sphere_row(const KIkcProg<T>& P, uint32_t anc, T px, T py, T pz, const T (&g)[3],
+                                           const T (&rz)[MAXV][3], const T (&rm)[MAXV][3], const T (&b)[3],
+                                           T (&av)[MAXV]) {
+    const T w0 = fma(py, g[2], -(pz * g[1]));
+    const T w1 = fma(pz, g[0], -(px * g[2]));
+    const T w3 = fma(px, g[1], -(py * g[0]));
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        T x;
+        if (v == P.base_col) x = g[0];
+        else if (v == P.base_col + 1) x = g[1];
+        else if (P.base_col >= 0 && v == P.base_col + 2) x = fma(-g[0], py - b[1], g[1] * (px - b[0]));
+        else if ((P.prism_mask >> v) & 1u) x = fma(g[0], rz[v][0], fma(g[1], rz[v][1], g[2] * rz[v][2]));
+        else
+            x = fma(rz[v][0], w0, fma(rz[v][1], w1, fma(rz[v][2], w3,
+                    -fma(g[0], rm[v][0], fma(g[1], rm[v][1], g[2] * rm[v][2])))));
+        av[v] = ((anc >> v) & 1u) ? x : T(0);
+    }
+}
+
+// w^2 a a^T and w^2 viol a into the lower triangle of the normal equations, over the variables of anc
+template <typename T, int MAXV>
+__device__ __forceinline__ void accum_row(T (&A)[MAXV][MAXV], T (&bv)[MAXV], const T (&av)[MAXV], T viol, T w2,
+                                          uint32_t anc) {
+#pragma unroll
+    for (int r = 0; r < MAXV; ++r) {
+        if (!((anc >> r) & 1u)) continue;
+        const T wr = w2 * av[r];
+        bv[r] = fma(wr, viol, bv[r]);
+#pragma unroll
+        for (int c = 0; c <= r; ++c)
+            if ((anc >> c) & 1u) A[r][c] = fma(wr, av[c], A[r][c]);
+    }
+}
+
+// min over the S lanes of an aligned group (S <= 16, inside one DPP row): quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror -- every lane ends with the same value
+template <int S>
+__device__ __forceinline__ float row_group_min(float v) {
+    if constexpr (S >= 2) v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    if constexpr (S >= 4) v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    if constexpr (S >= 8) v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false)));
+    if constexpr (S >= 16) v = fminf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false)));
+    return v;
+}
+template <int CTL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int S>
+__device__ __forceinline__ double row_group_min(double v) {
+    if constexpr (S >= 2) v = fmin(v, dpp_f64<0xB1>(v));
+    if constexpr (S >= 4) v = fmin(v, dpp_f64<0x4E>(v));
+    if constexpr (S >= 8) v = fmin(v, dpp_f64<0x141>(v));
+    if constexpr (S >= 16) v = fmin(v, dpp_f64<0x140>(v));
+    return v;
+}
+
+// value of lane `src` (inside the caller's lane group) for every lane of the group: ds_bpermute
+__device__ __forceinline__ float lane_bcast(float v, int src) { return __int_as_float(__shfl(__float_as_int(v), src)); }
+__device__ __forceinline__ double lane_bcast(double v, int src) { return __shfl(v, src); }
+
+// min over the G attempt groups of a target (lanes S apart): DPP inside a quad for S = 1, else
+// ds_bpermute (once per iteration)
+template <int G, int S>
+__device__ __forceinline__ int attempt_min(int v) {
+    if constexpr (S == 1) {
+        return group_min<G>(v);
+    } else {
+#pragma unroll
+        for (int w = S; w < G * S; w <<= 1) v = min(v, __shfl_xor(v, w));
+        return v;
+    }
+}
+template <int G, int S, typename T>
+__device__ __forceinline__ T attempt_min_t(T v) {
+#pragma unroll
+    for (int w = S; w < G * S; w <<= 1) v = fmin(v, __shfl_xor(v, w));
+    return v;
+}
+
+// starting angles of an attempt: attempt 0 from q0; attempt k >= 1 re-draws every free joint variable
+// within its limits (U[-pi, pi] if unbounded) from the counter hash of k_ik_dls (ik_seed_u01), other
+// variables from q0 (the base is reset by the caller)
+template <typename T, int MAXV>
+__device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>& a, const T* __restrict__ q,
+                                          int64_t ldq, uint32_t off, int64_t gi, int att, T (&qs)[MAXV]) {
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        if (v >= P.n_q) {
+            qs[v] = T(0);
+            continue;
+        }
+        if (att > 0 && ((P.free_mask & P.joint_mask) >> v) & 1u) {
+            double lo = (double)P.vlo[v], hi = (double)P.vhi[v];
+            if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
+            qs[v] = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, v));
+        } else {
+            qs[v] = ld_soa(q, v, ldq, off);
+        }
+    }
+}
+
+// k_ik_tree.  Lanes: G attempt groups of S lanes per target (G * S <= 64, aligned).  Lane group `ga`
+// of a target runs attempts ga, ga + G, ... of k_ik_dls's restart schedule; a group stops once a
+// lower attempt of its target has converged.  The S lanes of a group evaluate the same iteration:
+// every lane walks the tree (the chain is short), the spheres are shared out (lane j takes spheres j,
+// j + S, ...: its sphere's UnionSDF distance, analytic gradient and IneqConst row), and the sphere
+// rows enter the normal equations in sphere order, broadcast from their lane -- the same operations
+// in the same order as one lane doing every sphere (S = 1), so the results are identical for every
+// S and G.  Per iteration ONE damped Gauss-Newton step on the normal equations over the free
+// variables:
+//     (J^T J + w^2 sum_k a_k^T a_k + lambda^2 I) dq = J^T e + w^2 sum_k a_k^T (margin + band - d_k)
+// over the spheres with d_k < margin + band (a one-sided penalty: it pushes only while a sphere is
+// too close, so in the null space of the pose task the arm moves out to the band while the pose
+// error goes to zero); converged when |dp| < tol_pos, |rot| < tol_rot and every d_k >= margin - feas.
+// Joint limits: a joint on a limit pushed further out (by this step if it was free, by the right-hand
+// side if it was held) is held out of the next step; q is clamped to the limits.  Output: the lowest
+// converged attempt, else the attempt whose end state has the lowest merit
+// |dp|^2 + |rot|^2 + w^2 max(0, margin - min_k d_k)^2 (ties: the lower attempt) -- NLopt likewise
+// returns the best point it found.  NR: rounds of spheres per lane (ceil(n_sph / S); S > 1 only in
+// the specialised kernels, where the program is constant).  MAXG > 0: boxes attached to a scene,
+// one set of scene joint values per target (sa).
+template <typename T, int MAXV, int ROWS, int G, int S, int NR, int MAXG>
+__device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>* __restrict__ St,
+                                         const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
+                                         const CollArgs& ca, const IkcArgsT<T>& cz, const IkArgsT<T>& a,
+                                         const SceneArgs<T>& sa, const T* __restrict__ tgt, int64_t ldt,
+                                         T* __restrict__ q, int64_t ldq, int64_t n, int32_t* __restrict__ iters,
+                                         T* __restrict__ err, int64_t lde, unsigned char* smem) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "attempt groups");
+    static_assert(S == 1 || S == 2 || S == 4 || S == 8 || S == 16, "sphere lanes inside a DPP row");
+    static_assert(G * S <= 64 && MAXV <= kIkcMaxVars, "lane groups inside a wave");
+    const bool use_lds = ca.n_boxes <= kCollLdsBoxes;  // argmin box gathers from LDS (k_coll)
+    if (use_lds) {
+        const int words = ca.n_boxes * (int)(sizeof(KBox<T>) / 16);
+        for (int w = (int)threadIdx.x; w < words; w += (int)blockDim.x)
+            reinterpret_cast<uint4*>(smem)[w] = reinterpret_cast<const uint4*>(boxes)[w];
+        __syncthreads();
+    }
+    const uint64_t gi = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / (G * S);
+    const int lane = (int)(threadIdx.x & 63u);
+    const int sl = lane % S;                // sphere lane inside the attempt group
+    const int ga = (lane / S) % G;          // attempt group
+    const int gbase = lane - sl;            // first lane of this attempt group
+    if (gi >= (uint64_t)n) return;          // (whole targets: blockDim is a multiple of G * S)
+    const uint32_t off = (uint32_t)gi * (uint32_t)sizeof(T);
+    const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + ca.n_boxes);
+    const bool base = P.base_col >= 0;
+    const T* __restrict__ qin = a.q0 ? a.q0 : q;
+
+    T Rt[9], pt[3], trpy[3] = {T(0), T(0), T(0)};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Rt[3 * r + c] = ld_soa(tgt, r + 3 * c, ldt, off);
+        pt[r] = ld_soa(tgt, 9 + r, ldt, off);
+    }
+    if (ROWS == 6 && a.rpy_obj) {
+        T kk[6];
+        rpy_and_rate(Rt, trpy, kk);
+    }
+    // the scene state of this target (boxes attached to a scene mechanism): fixed during the solve
+    constexpr int MG = MAXG > 0 ? MAXG : 1;
+    SceneCtx<T, MG> sc;
+    if constexpr (MAXG > 0) scene_frames(sc, sa, off);
+    T b0[3] = {T(0), T(0), T(0)};
+    if (base)
+        for (int k = 0; k < 3; ++k) b0[k] = ld_soa(qin, P.base_col + k, ldq, off);
+    T qs[MAXV], b[3] = {b0[0], b0[1], b0[2]};
+    const int L = a.attempt_len;
+    int att = ga, it = ga > 0 ? ga * L + 1 : 0;  // attempt 0 from q0 at iteration 0, k >= 1 re-drawn at kL + 1
+    ikt_start<T, MAXV>(P, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
+    uint32_t held = 0;  // bit v: variable v held out of the step
+    bool conv = false;
+    bool done = att >= a.n_attempts;  // (groups beyond the schedule's attempts)
+    int res_att = INT_MAX;            // this group's converged attempt
+    // best attempt end so far (merit, attempt, state) for the no-convergence output
+    T best_m = T(INFINITY), bq[MAXV], bb[3] = {T(0), T(0), T(0)}, bep = T(0), ber = T(0), bdm = T(0);
+    int best_att = INT_MAX;
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) bq[v] = qs[v];
+    T ep = T(0), er = T(0), dmin = T(INFINITY);
+    const T w2 = cz.weight * cz.weight;
+    const T act = cz.margin + cz.band;
+    const uint32_t active = P.free_mask;
+    auto sdf_at = [&](T px, T py, T pz, T& d, T (&g)[3]) {  // the union (static or attached) at one point
+        T xs[1] = {px}, ys[1] = {py}, zs[1] = {pz}, ds[1], gs[1][3];
+        if constexpr (MAXG > 0) scene_union<T, true, 1, MG>(sc, boxes, aabb, xs, ys, zs, ds, gs, smem, use_lds);
+        else union_sdf<T, true, 1>(boxes, aabb, ca.n_aabb, ca.n_boxes, xs, ys, zs, ds, gs, smem, use_lds);
+        d = ds[0];
+        g[0] = gs[0][0]; g[1] = gs[0][1]; g[2] = gs[0][2];
+    };
+    for (;;) {
+        if constexpr (G > 1 || S > 1) {  // every lane of the wave is here: the loop exits wave-wide
+            if constexpr (G > 1) {
+                const int gm = attempt_min<G, S>(res_att);  // lowest converged attempt of the target so far
+                if (!done && gm < att) done = true;
+            }
+            if (__ballot(!done) == 0) break;
+        } else {
+            if (done) break;
+        }
+        if (done) continue;
+        // ---- tree walk: frames, joint records, spheres ----------------------------------------------
+        Fr<T> root;
+        if (base) base_frame(root, b[0], b[1], b[2]);
+        else set_identity(root);
+        Fr<T> cur = root, Lf = root, slot[kIkcMaxSlots];
+        T rz[MAXV][3], rm[MAXV][3];
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) rz[v][k] = rm[v][k] = T(0);
+        T A[MAXV][MAXV], bv[MAXV];  // lower triangle of the normal equations, right-hand side
+#pragma unroll
+        for (int r = 0; r < MAXV; ++r) {
+            bv[r] = T(0);
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) A[r][c] = T(0);
+        }
+        dmin = T(INFINITY);
+        // S > 1: this lane's sphere of each round (centre, radius, the variables moving it)
+        T pc[NR > 0 ? NR : 1][3], prad[NR > 0 ? NR : 1];
+        uint32_t panc[NR > 0 ? NR : 1];
+        if constexpr (S > 1) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                pc[r][0] = pc[r][1] = pc[r][2] = T(0);
+                prad[r] = T(0);
+                panc[r] = 0u;
+            }
+        }
+        auto spheres = [&](const Fr<T>& f, int k0, int k1) {
+            KIN_IKT_UNROLL
+            for (int k = k0; k < k1; ++k) {
+                const KSphere<T>& sp = sph[k];
+                const uint32_t anc = sp.anc;
+                const T px = fmz(f.r[0], sp.c[0], fmz(f.r[1], sp.c[1], fmz(f.r[2], sp.c[2], f.t[0])));
+                const T py = fmz(f.r[3], sp.c[0], fmz(f.r[4], sp.c[1], fmz(f.r[5], sp.c[2], f.t[1])));
+                const T pz = fmz(f.r[6], sp.c[0], fmz(f.r[7], sp.c[1], fmz(f.r[8], sp.c[2], f.t[2])));
+                if constexpr (S == 1) {  // evaluated in the walk, rows into the system at once
+                    T dr, g[3];
+                    sdf_at(px, py, pz, dr, g);
+                    const T d = dr - sp.r;
+                    dmin = fmin(dmin, d);
+                    const T viol = act - d;
+                    if (viol > T(0)) {  // divergent: this lane's sphere is inside the band
+                        T av[MAXV];
+                        sphere_row<T, MAXV>(P, anc, px, py, pz, g, rz, rm, b, av);
+                        accum_row<T, MAXV>(A, bv, av, viol, w2, anc);
+                    }
+                } else {  // kept by the lane that owns the sphere (k % S), evaluated after the walk
+                    const int r = k / S;
+                    if (k % S == sl) {
+#pragma unroll
+                        for (int rr = 0; rr < NR; ++rr)
+                            if (rr == r) {
+                                pc[rr][0] = px; pc[rr][1] = py; pc[rr][2] = pz;
+                                prad[rr] = sp.r;
+                                panc[rr] = anc;
+                            }
+                    }
+                }
+            }
+        };
+        spheres(root, P.sph_root0, P.sph_root1);
+        KIN_IKT_UNROLL
+        for (int s = 0; s < P.nS; ++s) {
+            const KIkcStep<T>& st = St[s];
+            if (st.parent == kIkcRoot) cur = root;
+            else if (st.parent >= 0) pick_frame(cur, slot, st.parent);
+            mul_rigid(cur, st.F);
+            // _get_joint_axis (src/algorithm.jl:42-54): pre-motion world axis z and m = z x o
+            const T sc0 = st.scale;
+            const T zx = cur.r[2] * sc0, zy = cur.r[5] * sc0, zz = cur.r[8] * sc0;
+            const T ox = cur.t[0], oy = cur.t[1], oz = cur.t[2];
+#pragma unroll
+            for (int v = 0; v < MAXV; ++v)
+                if (v == st.var) {
+                    rz[v][0] = zx; rz[v][1] = zy; rz[v][2] = zz;
+                    rm[v][0] = fma(zy, oz, -(zz * oy));
+                    rm[v][1] = fma(zz, ox, -(zx * oz));
+                    rm[v][2] = fma(zx, oy, -(zy * ox));
+                }
+            motion<T, true>(cur, st.kind, st.flags, sc0, pick(qs, st.var));  // fast trig (fp32)
+            if (st.save >= 0) put_frame(slot, st.save, cur);
+            spheres(cur, st.sph0, st.sph1);
+            if (s == P.tgt_step) Lf = cur;
+        }
+        link_frame(Lf, Lf, P.has_xt != 0, P.Xt);
+        if constexpr (S > 1) {
+            // this lane's spheres: distance, gradient, row; then every in-band row into the system in
+            // sphere order, broadcast from its lane
+            T av[NR][MAXV], viol[NR];
+            uint64_t inband[NR];
+            T dl = T(INFINITY);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const bool valid = r * S + sl < P.n_sph;
+                T dr, g[3];
+                sdf_at(pc[r][0], pc[r][1], pc[r][2], dr, g);
+                const T d = dr - prad[r];
+                dl = valid ? fmin(dl, d) : dl;
+                viol[r] = act - d;
+                const bool inb = valid && viol[r] > T(0);
+                sphere_row<T, MAXV>(P, panc[r], pc[r][0], pc[r][1], pc[r][2], g, rz, rm, b, av[r]);
+                inband[r] = __ballot(inb);
+            }
+            dmin = row_group_min<S>(dl);
+            KIN_IKT_UNROLL
+            for (int k = 0; k < P.n_sph; ++k) {
+                const int r = k / S, src = gbase + k % S;
+                const uint32_t anc = sph[k].anc;  // (constant in the specialised kernel)
+                uint64_t bal = 0;
+#pragma unroll
+                for (int rr = 0; rr < NR; ++rr)
+                    if (rr == r) bal = inband[rr];
+                if ((bal >> src) & 1ull) {  // (uniform inside the attempt group)
+                    T vk = T(0), ak[MAXV];
+#pragma unroll
+                    for (int rr = 0; rr < NR; ++rr)
+                        if (rr == r) {
+                            vk = lane_bcast(viol[rr], src);
+#pragma unroll
+                            for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? lane_bcast(av[rr][v], src) : T(0);
+                        }
+                    accum_row<T, MAXV>(A, bv, ak, vk, w2, anc);
+                }
+            }
+        }
+        // ---- pose error, convergence, attempt ends ---------------------------------------------------
+        T e[6];
+        e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
+        ep = sqrt_fast(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        er = T(0);
+        T kr[6];
+        if constexpr (ROWS == 6) {
+            T w[3];
+            if (a.rpy_obj) {
+                T r[3];
+                rpy_and_rate(Lf.r, r, kr);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) w[k] = wrap_pi(trpy[k] - r[k]);
+            } else {
+                rot_error(Rt, Lf.r, w);
+            }
+            e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
+            er = sqrt_fast(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        }
+        if (ep < a.tol_pos && er < a.tol_rot && dmin >= cz.margin - cz.feas) {
+            conv = true;
+            res_att = att;
+            done = true;
+            continue;
+        }
+        const bool last = it >= a.max_iters;  // (only the last attempt gets here)
+        const bool over = !last && L > 0 && it > 0 && it % L == 0;
+        if (last || over) {  // an attempt ends here: keep it if it is the best end state so far
+            const T vm = fmax(cz.margin - dmin, T(0));
+            T m = fma(w2 * vm, vm, fma(ep, ep, er * er));
+            m = m == m ? m : T(INFINITY);  // (NaN: worst)
+            if (m < best_m || best_att == INT_MAX) {
+                best_m = m;
+                best_att = att;
+#pragma unroll
+                for (int v = 0; v < MAXV; ++v) bq[v] = qs[v];
+                bb[0] = b[0]; bb[1] = b[1]; bb[2] = b[2];
+                bep = ep; ber = er; bdm = dmin;
+            }
+            if (last) {
+                done = true;
+                continue;
+            }
+            att += G;  // this group's next attempt, re-drawn
+            if (att >= a.n_attempts) {
+                done = true;
+                continue;
+            }
+            it = att * L + 1;
+            ikt_start<T, MAXV>(P, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
+            b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
+            held = 0;
+            continue;
+        }
+        // ---- pose rows: J^T J and J^T e ---------------------------------------------------------------
+        // row r of J over the variables: revolute [z x p - m; z], prismatic [z; 0], base [1 0 -y'; 0 1 x'; ..]
+        // (p' = p - base); with the reference objective the angular rows are d(rpy)/dq.  Accumulated row by
+        // row (12 values live), each entry's FMAs in row order.
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            T Jr[MAXV];
+#pragma unroll
+            for (int v = 0; v < MAXV; ++v) {
+                Jr[v] = T(0);
+                if (!((P.tgt_mask >> v) & 1u)) continue;
+                if (base && v >= P.base_col) {
+                    const int k = v - P.base_col;
+                    if (k == 0) Jr[v] = r == 0 ? T(1) : T(0);
+                    else if (k == 1) Jr[v] = r == 1 ? T(1) : T(0);
+                    else Jr[v] = r == 0 ? -(Lf.t[1] - b[1]) : r == 1 ? Lf.t[0] - b[0] : r == 5 ? T(1) : T(0);
+                    continue;
+                }
+                const T x = rz[v][0], y = rz[v][1], z = rz[v][2];
+                if ((P.prism_mask >> v) & 1u) {
+                    Jr[v] = r == 0 ? x : r == 1 ? y : r == 2 ? z : T(0);
+                    continue;
+                }
+                if (r == 0) Jr[v] = fma(y, Lf.t[2], -fma(z, Lf.t[1], rm[v][0]));
+                else if (r == 1) Jr[v] = fma(z, Lf.t[0], -fma(x, Lf.t[2], rm[v][1]));
+                else if (r == 2) Jr[v] = fma(x, Lf.t[1], -fma(y, Lf.t[0], rm[v][2]));
+                else if (a.rpy_obj) Jr[v] = r == 3 ? fma(kr[0], x, kr[1] * y) : r == 4 ? fma(kr[2], x, kr[3] * y)
+                                                                            : fma(kr[4], x, fma(kr[5], y, z));
+                else Jr[v] = r == 3 ? x : r == 4 ? y : z;
+            }
+#pragma unroll
+            for (int v = 0; v < MAXV; ++v) {
+                if (!((P.tgt_mask >> v) & 1u)) continue;
+                bv[v] = fma(Jr[v], e[r], bv[v]);
+#pragma unroll
+                for (int c = 0; c <= v; ++c)
+                    if ((P.tgt_mask >> c) & 1u) A[v][c] = fma(Jr[v], Jr[c], A[v][c]);
+            }
+        }
+        // ---- the step --------------------------------------------------------------------------------
+        const uint32_t freev = active & ~held;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            const bool fv = (freev >> v) & 1u;
+#pragma unroll
+            for (int c = 0; c < v; ++c)
+                if (!fv || !((freev >> c) & 1u)) A[v][c] = T(0);
+            A[v][v] = fv ? A[v][v] + a.lam2 : T(1);
+        }
+        T y[MAXV];
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) y[v] = ((freev >> v) & 1u) ? bv[v] : T(0);
+        // Cholesky (in place, lower) and the two triangular solves
+#pragma unroll
+        for (int j = 0; j < MAXV; ++j) {
+            T d = A[j][j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) d = fma(-A[j][k], A[j][k], d);
+            d = sqrt_t(d);
+            A[j][j] = d;
+            const T id = T(1) / d;
+#pragma unroll
+            for (int r = j + 1; r < MAXV; ++r) {
+                T sm = A[r][j];
+#pragma unroll
+                for (int k = 0; k < j; ++k) sm = fma(-A[r][k], A[j][k], sm);
+                A[r][j] = sm * id;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < MAXV; ++r) {
+            T sm = y[r];
+#pragma unroll
+            for (int k = 0; k < r; ++k) sm = fma(-A[r][k], y[k], sm);
+            y[r] = sm / A[r][r];
+        }
+#pragma unroll
+        for (int r = MAXV - 1; r >= 0; --r) {
+            T sm = y[r];
+#pragma unroll
+            for (int k = r + 1; k < MAXV; ++k) sm = fma(-A[k][r], y[k], sm);
+            y[r] = sm / A[r][r];
+        }
+        T mx = T(0);
+        uint32_t nh = 0;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            if (!((active >> v) & 1u)) continue;
+            if ((P.joint_mask >> v) & 1u) {
+                const bool was = (held >> v) & 1u;
+                const T dir = was ? bv[v] : y[v];  // held: the descent direction J^T e + ...
+                if ((qs[v] <= P.vlo[v] && dir < T(0)) || (qs[v] >= P.vhi[v] && dir > T(0))) nh |= 1u << v;
+                if (was) y[v] = T(0);
+            }
+            mx = fmax(mx, fabs(y[v]));
+        }
+        held = nh;
+        const T sc = mx > a.max_step ? a.max_step / mx : T(1);
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            if (!((active >> v) & 1u)) continue;
+            if ((P.joint_mask >> v) & 1u) qs[v] = fmin(fmax(fma(sc, y[v], qs[v]), P.vlo[v]), P.vhi[v]);
+            else if (base && v >= P.base_col) {
+                const int k = v - P.base_col;
+                const T nb = fma(sc, y[v], b[k]);
+                b[0] = k == 0 ? nb : b[0];
+                b[1] = k == 1 ? nb : b[1];
+                b[2] = k == 2 ? nb : b[2];
+            }
+        }
+        ++it;
+    }
+    // ---- outputs: the lowest converged attempt, else the best attempt end ----------------------------
+    bool write = true;
+    if constexpr (G > 1) {
+        const int gm = attempt_min<G, S>(res_att);
+        if (gm != INT_MAX) {
+            write = res_att == gm;
+        } else {
+            const T mm = attempt_min_t<G, S>(best_m);
+            const int am = attempt_min<G, S>(best_m == mm ? best_att : INT_MAX);
+            write = best_att == am;
+        }
+    }
+    if (!write || sl != 0) return;
+    if (!conv) {
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) qs[v] = bq[v];
+        b[0] = bb[0]; b[1] = bb[1]; b[2] = bb[2];
+        ep = bep; er = ber; dmin = bdm;
+    }
+    for (int v = 0; v < P.n_q; ++v) st_soa(q, v, ldq, off, pick(qs, v));
+    if (base)
+        for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
+    if (iters) iters[gi] = conv ? it : a.max_iters + 1;
+    if (err) {
+        st_soa(err, 0, lde, off, ep);
+        st_soa(err, 1, lde, off, er);
+        st_soa(err, 2, lde, off, dmin);
+    }
+}
+
+}  // namespace
+}  // namespace kinhip
+
+#pragma clang fp contract(fast)  // (the translation unit's default again: -ffp-contract=fast-honor-pragmas)

@@ -55,8 +55,14 @@ struct JitFns {
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
     hipFunction_t coll_scene[2][2] = {};  // the same over an attached union [with gradients][up to 2 | 4 groups]
-    hipFunction_t ikc[2][2] = {};  // collision-aware IK [rows == 6][kIkcLanes lanes per target]
+    // collision-aware IK (k_ik_tree) [rows == 6][lanes: 0 = 1 x 1, 1 = 1 sphere lane x 4 attempt groups,
+    // 2 = 16 sphere lanes x 1, 3 = 16 x 4] (kIktVariants)
+    hipFunction_t ikt[2][4] = {};
 };
+// sphere lanes S and attempt groups G of the specialised k_ik_tree kernels, by JitFns::ikt index
+constexpr int kIktVariants = 4;
+constexpr int kIktS[kIktVariants] = {1, 1, 16, 16};
+constexpr int kIktG[kIktVariants] = {1, 4, 1, 4};
 
 // jf: the plan-specialised kernels (kinhip_jit.cpp) or null for the generic one
 template <typename T>
@@ -96,17 +102,18 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
                          const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
                          T* err, int64_t lde, const JitFns* jf, const IkScratch& scr, hipStream_t st);
 
-// collision-aware IK (k_ik_coll, kinhip_ikc_dev.h): sphere-distance bound and penalty rows
+// collision-aware IK (k_ik_tree, kinhip_ikt_dev.h): sphere-distance bound and penalty rows
 struct IkcArgs {
     double margin, band, weight, feas;
 };
-constexpr int kIkcMaxChain = 8;  // generic k_ik_coll kernels: chains of <= 8 steps
+struct SceneLaunch;
 
+// scene: boxes attached to a scene mechanism, scene joint values per target (null: a static union)
 template <typename T>
-hipError_t launch_ik_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
-                          const LaunchGeom& g, const CollArgs& ca, const IkcArgs& c, const IkArgs& a, const T* target,
-                          int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters, T* err, int64_t lde,
-                          const JitFns* jf, hipStream_t st);
+hipError_t launch_ik_tree(const KIkcProg<T>& P, const KIkcStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
+                          const CollArgs& ca, const SceneLaunch* scene, const IkcArgs& c, const IkArgs& a,
+                          const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
+                          T* err, int64_t lde, const JitFns* jf, hipStream_t st);
 
 template <typename T>
 hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* pts,

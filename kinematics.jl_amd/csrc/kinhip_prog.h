@@ -40,8 +40,6 @@ enum : int32_t { PF_JAC = 1, PF_WITH_ROT = 2, PF_RPY = 4, PF_ZERO = 8, PF_BASE =
 // The IK kernels take kIkChunk per launch.
 constexpr int64_t kChunk = int64_t(1) << 27;
 constexpr int64_t kIkChunk = kChunk / 8;
-// lanes per target of the parallel-attempt collision-aware IK kernel (k_ik_coll, ikc_group)
-constexpr int kIkcLanes = 4;
 // two-phase IK hand-over rings (IkArgsT, kinhip_ik_dev.h): one per lane of a wave (the phase-2 prefix
 // scan), their control words one 128-byte line apart
 constexpr int kIkSubRings = 64;
@@ -77,8 +75,9 @@ template <typename T>
 struct KSphere {
     T c[3];
     T r;
-    int32_t out;  // output row (the caller's sphere order)
-    int32_t pad[3];
+    int32_t out;   // output row (the caller's sphere order)
+    uint32_t anc;  // collision-aware IK programs: the variables moving the sphere (KIkcStep::anc)
+    int32_t pad[2];
 };
 
 // one BoxSDF of a UnionSDF (src/sdf.jl:48-114): inverse world pose (row-major
@@ -124,6 +123,53 @@ struct KSceneGroup {
     int32_t pad[2];
 };
 constexpr int kMaxSceneGroups = 4;  // moving frames carrying boxes (per-lane frames in registers)
+
+// ---- collision-aware IK program (kin_coll_ik_plan_create, k_ik_tree, kinhip_ikt_dev.h) ----
+// The needed kinematic tree -- every moving joint above the target link or above a sphere link, in
+// depth-first order -- as one step per moving joint:
+//     C <- C_parent * F;  record z = scale * C e_z, m = z x C.t (pre-motion world joint axis, origin);
+//     C <- C * motion(q[var]);  [save C to slot `save`]
+// C_parent is the previous step's frame (parent == kIkcPrev), the root / planar-base frame
+// (kIkcRoot), or a saved branch frame (slot parent >= 0).  Static chains (fixed joints, joints held at
+// m.angles) are folded into F on the host in fp64 as joint_transform does (src/mechanism.jl:90-103);
+// frames are canonical (the joint axis on local z) as in KStep.  Spheres hang off a step's
+// post-motion frame (or the root frame); the target link's frame is frame(tgt_step) * Xt.
+constexpr int kIkcMaxVars = 12;   // q columns + 3 base columns (normal equations in registers)
+constexpr int kIkcMaxSteps = 32;  // moving joints on the needed tree
+constexpr int kIkcMaxSlots = 2;   // saved branch frames live at once
+constexpr int kIkcMaxSpheres = 64;
+constexpr int32_t kIkcPrev = -1, kIkcRoot = -2;
+template <typename T>
+struct KIkcStep {
+    T F[12];   // row-major 3x4
+    T scale;   // |axis| (revolute angle map / prismatic slide / record scale)
+    T pad[3];
+    int32_t kind;    // MOT_REV / MOT_PRISM
+    int32_t flags;   // SF_SCALE
+    int32_t var;     // variable (q column) driving the joint
+    int32_t parent;  // kIkcPrev, kIkcRoot or a slot
+    int32_t save;    // slot receiving the post-motion frame (-1: none)
+    int32_t sph0, sph1;  // spheres [sph0, sph1) on the post-motion frame
+    uint32_t anc;    // variables moving this frame: the joints above it (and itself), the base
+};
+template <typename T>
+struct KIkcProg {
+    int32_t nS;         // steps
+    int32_t nv;         // variables: n_q joint columns, then base x, y, theta (base_col) if with_base
+    int32_t n_q;
+    int32_t base_col;   // -1: no planar base
+    int32_t n_sph;
+    int32_t sph_root0, sph_root1;  // spheres on the root (base) frame
+    int32_t tgt_step;   // step whose frame carries the target link (kIkcRoot: the root frame)
+    int32_t has_xt;
+    uint32_t tgt_mask;  // variables moving the target link (pose Jacobian columns)
+    uint32_t free_mask; // variables the solver moves (they move the target or a sphere)
+    uint32_t joint_mask;  // variables that are joints (a step records them)
+    uint32_t prism_mask;  // joint variables that slide (prismatic Jacobian column)
+    int32_t pad;
+    T Xt[12];           // target link frame = frame(tgt_step) * Xt
+    T vlo[kIkcMaxVars], vhi[kIkcMaxVars];  // joint limits of the variables (base: +-inf)
+};
 
 // kernel-side tiling: workgroup b works on tile b / tile_blocks (0xffffffff: plain SoA)
 struct Tiling {

@@ -38,7 +38,8 @@ EXPORTS = [
     "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch", "kin_coll_batch_tiled",
     "kin_ineq_const_batch", "kin_ineq_const_batch_tiled", "kin_pose_const_batch",
-    "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_sdf_create_attached", "kin_coll_batch_scene",
+    "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
+    "kin_coll_batch_scene",
 ]
 
 
@@ -138,6 +139,7 @@ def lib():
         "kin_sdf_create_attached": ([P, I32, P, I32, P, P, P, P], C.c_int),
         "kin_coll_batch_scene": ([P, P, C.c_double, P, I64, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
         "kin_ik_coll_batch": ([P, P, P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
+        "kin_ik_coll_batch_scene": ([P, P, P, P, P, I64, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -244,10 +244,10 @@ CollisionPlan._run_scene = _run_scene
 
 
 class CollisionIKPlan(Plan):
-    """kin_coll_ik_plan_create: the IK plan of `link` over `joints` with the checker's spheres staged on
-    the same chain -- both stages of inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
-    (src/inverse_kinematics.jl:1-21) for many targets per launch (``solve``).  It is also an ordinary IK
-    plan (``ik_dls``)."""
+    """kin_coll_ik_plan_create: the IK plan of `link` over `joints` with the tree of the target link and the
+    checker's spheres (on any chain: both arms, torso, head) -- both stages of inverse_kinematics!(m, link,
+    joints, target, sscc, sdf; use_bistage) (src/inverse_kinematics.jl:1-21) for many targets per launch
+    (``solve``).  It is also an ordinary IK plan (``ik_dls``)."""
 
     def __init__(self, sscc: SweptSphereCollisionChecker, link: Link, joints, dtype=torch.float32):
         m = sscc.mech
@@ -278,13 +278,16 @@ class CollisionIKPlan(Plan):
         K.check(K.lib().kin_plan_specialize(self._h, int(kernels) or (K.KIN_SPEC_IK | K.KIN_SPEC_IK_COLL)))
         return self
 
-    def ik_coll(self, sdf: UnionSDF, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
+    def ik_coll(self, sdf, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
                 margin=0.02, band=0.0, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-                max_step=0.5, with_rot=2, restarts=0, seed=0, lanes=0, index_base=0, stream=None):
+                max_step=0.5, with_rot=2, restarts=0, seed=0, lanes=0, index_base=0, stream=None,
+                scene_q: Optional[torch.Tensor] = None):
         """Stage 2 alone (kin_ik_coll_batch): from Q0 (or Q in place) -> (Q, iters [N], err [3, N]:
-        |dp|, |rot|, min sphere distance).  iters > max_iters: not converged.  `lanes`: 0 = auto (restart
-        attempts side by side on 4 lanes per target for small batches), 1 = attempts in sequence on one
-        lane; the results do not depend on it."""
+        |dp|, |rot|, min sphere distance).  iters > max_iters: not converged (Q, err: the attempt with the
+        best end state).  `lanes`: 0 = auto (restart attempts side by side and spheres shared out over lanes
+        for small batches), 1 = attempts in sequence on one lane; the results do not depend on it.
+        With an ``AttachedUnionSDF`` (kin_ik_coll_batch_scene): `scene_q` = its scene columns per target
+        (n_scene_cols, N) or one vector (n_scene_cols,) for the batch."""
         N = self._check_q(Q)
         _plan_device(sdf, Q)
         if Q0 is not None:
@@ -300,12 +303,33 @@ class CollisionIKPlan(Plan):
                          int(restarts), int(seed), int(lanes), int(index_base))
         cp = K.IkCollParams(float(margin), float(band), float(weight), float(feas))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
-        K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
-                                          (Q0 if Q0 is not None else Q).data_ptr(), Q.data_ptr(), Q.stride(0), N,
-                                          iters.data_ptr(), err.data_ptr(), N, st))
+        q0p = (Q0 if Q0 is not None else Q).data_ptr()
+        if isinstance(sdf, AttachedUnionSDF):
+            if scene_q is None:
+                raise ValueError("an AttachedUnionSDF needs scene_q (its scene joint values)")
+            if scene_q.dtype != self.dtype:
+                raise ValueError("scene_q must have the plan dtype")
+            _same_device(scene_q, Q, "scene_q")
+            if scene_q.dim() == 1:
+                if scene_q.shape[0] != sdf.n_scene_cols or not scene_q.is_contiguous():
+                    raise ValueError(f"scene_q must hold {sdf.n_scene_cols} values")
+                lds = 0
+            else:
+                if scene_q.shape != (sdf.n_scene_cols, N) or scene_q.stride(1) != 1:
+                    raise ValueError(f"scene_q must be ({sdf.n_scene_cols}, N) with unit target stride")
+                lds = scene_q.stride(0)
+            K.check(K.lib().kin_ik_coll_batch_scene(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                                    scene_q.data_ptr() if scene_q.numel() else None, lds, q0p,
+                                                    Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N,
+                                                    st))
+            return Q, iters, err
+        if scene_q is not None:
+            raise ValueError("scene_q is only for an AttachedUnionSDF")
+        K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N, q0p,
+                                          Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N, st))
         return Q, iters, err
 
-    def solve(self, sdf: UnionSDF, targets: torch.Tensor, Q0: torch.Tensor, use_bistage=True, margin=0.02,
+    def solve(self, sdf, targets: torch.Tensor, Q0: torch.Tensor, use_bistage=True, margin=0.02,
               with_rot=2, max_iters=64, restarts=3, seed=0, index_base=0, stream=None, **kw):
         """Both stages on the device, no host round trip: stage 1 (use_bistage) = the collision-free
         DLS (kin_ik_dls_batch_from, the seeds read from Q0), stage 2 = kin_ik_coll_batch from its

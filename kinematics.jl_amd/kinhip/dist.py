@@ -38,7 +38,17 @@ def init_from_env(backend: Optional[str] = None, always_group: bool = False) -> 
     use_cuda = torch.cuda.is_available()
     dev = torch.device("cpu")
     if use_cuda:
-        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        ndev = torch.cuda.device_count()
+        if local >= ndev:
+            # one process per GPU: more local ranks than GPUs would silently double up GPUs.  Only the
+            # explicit gloo rehearsal (KINHIP_DIST_BACKEND=gloo: ranks sharing one GPU) may do that.
+            if backend != "gloo":
+                raise RuntimeError(f"LOCAL_RANK {local} >= {ndev} visible GPUs: launch one process per GPU "
+                                   f"(or set KINHIP_DIST_BACKEND=gloo to rehearse ranks sharing a GPU)")
+            local_dev = local % max(1, ndev)
+        else:
+            local_dev = local
+        dev = torch.device("cuda", local_dev)
         torch.cuda.set_device(dev)
     d, be = None, "none"
     if world > 1 or always_group:

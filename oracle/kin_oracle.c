@@ -869,13 +869,17 @@ void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, con
 
 /* ---- build-defined collision-aware IK (kin_ik_coll_batch), restated for parity ----
  * Stage 2 of inverse_kinematics!(m, link, joints, target, sscc, sdf) (src/inverse_kinematics.jl:1-21)
- * as the GPU kernel does it (kinhip_ikc_dev.h): per iteration the pose residual e (with_rot as in
+ * as the GPU kernel does it (kinhip_ikt_dev.h): per iteration the pose residual e (with_rot as in
  * or_ik_dls_batch) and, for every sphere with d_k < margin + band, the IneqConst row a_k = grad sdf^T J_k
  * (analytic gradient of the argmin box); one damped Gauss-Newton step on the normal equations
  *   (J^T J + w^2 sum a_k^T a_k + lambda^2 I) dq = J^T e + w^2 sum a_k^T (margin + band - d_k)
- * over the joints (+ base), joints held out while on a limit and pushed outward (by the last step, or by
- * the right-hand side while held), |dq|_inf <= max_step, clamp; converged when |dp| < tol_pos,
- * |rot| < tol_rot and every d_k >= margin - feas. */
+ * over the free variables -- the joints that move the target link or a sphere link (spheres may hang off
+ * any chain of the tree) and the base -- joints held out while on a limit and pushed outward (by the last
+ * step, or by the right-hand side while held), |dq|_inf <= max_step, clamp; converged when |dp| < tol_pos,
+ * |rot| < tol_rot and every d_k >= margin - feas.  Restarts as or_ik_dls_batch (every free joint
+ * re-drawn).  Not converged: the attempt whose end state has the lowest merit
+ * |dp|^2 + |rot|^2 + w^2 max(0, margin - min d)^2 (NaN = worst; ties: the earlier attempt).
+ * sdfs (optional): one union per target (boxes of a scene mechanism at that target's scene state). */
 static void box_gradient_analytic(const or_union_sdf* s, int32_t k, const double* p, double g[3]) {
     const double* T = s->inv_pose + 16 * k;
     double l[3], q[3], gl[3];
@@ -899,8 +903,8 @@ static void box_gradient_analytic(const or_union_sdf* s, int32_t k, const double
 
 void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, double* q, int64_t ldq, int32_t n_q,
                       const int32_t* qids, int32_t link_id, const double* target, int64_t ldt, const or_ik_params* prm,
-                      const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii, int32_t* iters_out,
-                      double* err_out, int32_t n_threads) {
+                      const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii,
+                      const or_union_sdf* const* sdfs, int32_t* iters_out, double* err_out, int32_t n_threads) {
     int nt = nthreads_of(n_threads);
     const int32_t nd = n_q + (proto->with_base ? 3 : 0);
     const int rows = prm->with_rot ? 6 : 3;
@@ -917,14 +921,25 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
         double* av = (double*)malloc(sizeof(double) * (nd + 1));
         double* lo = (double*)malloc(sizeof(double) * (nd + 1));
         double* hi = (double*)malloc(sizeof(double) * (nd + 1));
+        double* best = (double*)malloc(sizeof(double) * (nd + 1));
         int* rel = (int*)malloc(sizeof(int) * (nd + 1));
         for (int32_t c = 0; c < nd; ++c) {
-            rel[c] = c >= n_q || or_is_relevant(m, qids[c], link_id);
+            if (c >= n_q) {
+                rel[c] = 1;
+            } else {
+                const int32_t j = qids[c];
+                int r = m->jtype[j - 1] != OR_FIXED && or_is_relevant(m, j, link_id);
+                for (int32_t k = 0; k < n_sph && !r; ++k) r = m->jtype[j - 1] != OR_FIXED && or_is_relevant(m, j, sph[k]);
+                /* a repeated joint keeps its last column (set_joint_angles) */
+                for (int32_t c2 = c + 1; c2 < n_q && r; ++c2) if (qids[c2] == j) r = 0;
+                rel[c] = r;
+            }
             lo[c] = c < n_q && rel[c] ? m->jlower[qids[c] - 1] : -INFINITY;
             hi[c] = c < n_q && rel[c] ? m->jupper[qids[c] - 1] : INFINITY;
         }
 #pragma omp for schedule(static)
         for (int64_t i = 0; i < n; ++i) {
+            const or_union_sdf* sd = sdfs ? sdfs[i] : sdf;
             tf_t tgt = tf_identity();
             for (int k = 0; k < 12; ++k) tgt.m[(k / 3) * 4 + (k % 3)] = target[(size_t)k * ldt + i];
             double trpy[3];
@@ -932,11 +947,13 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
             for (int32_t c = 0; c < nd; ++c) a[c] = q[c * ldq + i];
             double a0[64];
             int held[64];
-            for (int32_t c = 0; c < nd; ++c) { a0[c] = a[c]; held[c] = 0; }
+            for (int32_t c = 0; c < nd; ++c) { a0[c] = a[c]; held[c] = 0; best[c] = a[c]; }
             const int32_t attempt_len = prm->restarts > 0 ? prm->max_iters / (prm->restarts + 1) : 0;
             int32_t it = 0;
             int conv = 0;
             double ep = 0, er = 0, dmin = INFINITY;
+            double best_m = INFINITY, bep = 0, ber = 0, bdm = 0;
+            int have_best = 0;
             for (;; ++it) {
                 or_set_joint_angles(m, n_q, qids, a);
                 memset(A, 0, sizeof(double) * nd * nd);
@@ -946,12 +963,12 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
                     tf_t t = get_transform(m, sph[k]);
                     double p[3] = {M(t, 0, 3), M(t, 1, 3), M(t, 2, 3)};
                     int32_t kb = 0;
-                    const double d = or_union_sdf_value(sdf, p, &kb) - radii[k];
+                    const double d = or_union_sdf_value(sd, p, &kb) - radii[k];
                     if (d < dmin) dmin = d;
                     const double viol = margin + band - d;
                     if (viol > 0) {
                         double g[3];
-                        box_gradient_analytic(sdf, kb, p, g);
+                        box_gradient_analytic(sd, kb, p, g);
                         memset(J3, 0, sizeof(double) * 3 * nd);
                         or_get_jacobian(m, sph[k], n_q, qids, 0, 0, J3);
                         for (int32_t c = 0; c < nd; ++c) av[c] = g[0] * J3[3 * c] + g[1] * J3[3 * c + 1] + g[2] * J3[3 * c + 2];
@@ -977,8 +994,18 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
                 ep = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
                 er = prm->with_rot ? sqrt(e[3] * e[3] + e[4] * e[4] + e[5] * e[5]) : 0.0;
                 if (ep < prm->tol_pos && er < prm->tol_rot && dmin >= margin - feas) { conv = 1; break; }
-                if (it >= prm->max_iters) break;
-                if (attempt_len > 0 && it > 0 && it % attempt_len == 0) {
+                const int last = it >= prm->max_iters;
+                const int over = !last && attempt_len > 0 && it > 0 && it % attempt_len == 0;
+                if (last || over) {  /* an attempt ends: keep its end state if it is the best so far */
+                    const double vm = margin - dmin > 0 ? margin - dmin : 0.0;
+                    double mr = w2 * vm * vm + (ep * ep + er * er);
+                    if (mr != mr) mr = INFINITY;
+                    if (mr < best_m || !have_best) {
+                        best_m = mr; have_best = 1;
+                        for (int32_t c = 0; c < nd; ++c) best[c] = a[c];
+                        bep = ep; ber = er; bdm = dmin;
+                    }
+                    if (last) break;
                     const int32_t att = it / attempt_len;
                     for (int32_t c = 0; c < nd; ++c) {
                         if (c < n_q && rel[c]) {
@@ -1022,15 +1049,20 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
                 }
                 const double sc = mx > prm->max_step ? prm->max_step / mx : 1.0;
                 for (int32_t c = 0; c < nd; ++c) {
+                    if (!rel[c]) continue;
                     const double v = a[c] + sc * y[c];
                     a[c] = v < lo[c] ? lo[c] : (v > hi[c] ? hi[c] : v);
                 }
+            }
+            if (!conv) {
+                for (int32_t c = 0; c < nd; ++c) a[c] = best[c];
+                ep = bep; er = ber; dmin = bdm;
             }
             for (int32_t c = 0; c < nd; ++c) q[c * ldq + i] = a[c];
             if (iters_out) iters_out[i] = conv ? it : prm->max_iters + 1;
             if (err_out) { err_out[i] = ep; err_out[n + i] = er; err_out[2 * n + i] = dmin; }
         }
-        free(a); free(J); free(J3); free(A); free(bv); free(y); free(av); free(lo); free(hi); free(rel);
+        free(a); free(J); free(J3); free(A); free(bv); free(y); free(av); free(lo); free(hi); free(best); free(rel);
         or_mech_destroy(m);
     }
 }

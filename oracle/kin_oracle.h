@@ -152,8 +152,8 @@ void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, con
  * cprm = {margin, band, weight, feas}; err_out [3][n]: |dp|, |rot|, min sphere distance. */
 void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, double* q, int64_t ldq, int32_t n_q,
                       const int32_t* qids, int32_t link_id, const double* target, int64_t ldt, const or_ik_params* prm,
-                      const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii, int32_t* iters_out,
-                      double* err_out, int32_t n_threads);
+                      const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii,
+                      const or_union_sdf* const* sdfs, int32_t* iters_out, double* err_out, int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -197,7 +197,7 @@ def lib():
         L.or_union_sdf_value.argtypes = [P, P, P]
         L.or_union_sdf_gradient.argtypes = [P, P, P]
         L.or_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, P, D, P, I64, P, I64, I32]
-        L.or_ik_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, I64, P, P, I32, P, P, P, P, I32]
+        L.or_ik_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, I64, P, P, I32, P, P, P, P, P, I32]
         _lib = L
     return _lib
 
@@ -344,22 +344,79 @@ class OracleMech:
 
 def ik_coll_batch(mech: "OracleMech", sdf: "OracleUnionSDF", q0, q_joint_ids, link_id, target, sphere_links, radii,
                   margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-                  max_step=0.5, with_rot=2, restarts=0, seed=0, n_threads=0):
-    """Restatement of kin_ik_coll_batch (stage 2 of the bistage collision-aware IK) -> (q, iters, err [3, N])."""
+                  max_step=0.5, with_rot=2, restarts=0, seed=0, n_threads=0, sdfs=None, sphere_parents=None):
+    """Restatement of kin_ik_coll_batch (stage 2 of the bistage collision-aware IK) -> (q, iters, err [3, N]).
+    `sdfs`: one OracleUnionSDF per target (a scene mechanism's boxes at each target's scene state) instead of
+    `sdf`.  `sphere_parents`: the tree links the sphere links hang off (add_new_link parents); with it the
+    sphere rows are added in the kernel's order (ikc_sphere_order) -- the same sums in the same order."""
     q = _f64(q0).copy()
     ids = _i32(q_joint_ids)
     tgt = _f64(target)
     sph = _i32(sphere_links)
     r = _f64(radii)
+    if sphere_parents is not None and sph.size:
+        order = ikc_sphere_order(mech.tree, ids, int(link_id), _i32(sphere_parents))
+        sph, r = _i32(sph[order]), _f64(r[order])
     N = q.shape[1]
     it = np.zeros(N, np.int32)
     err = np.zeros((3, N))
     prm = _IkParams(max_iters, lam, tol_pos, tol_rot, max_step, int(with_rot), int(restarts), int(seed))
     cp = _f64([margin, band, weight, feas])
-    lib().or_ik_coll_batch(mech._h, sdf._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt), tgt.shape[1],
-                           C.byref(prm), _p(cp), sph.size, _p(sph) if sph.size else None, _p(r) if sph.size else None,
+    harr = None
+    if sdfs is not None:
+        assert len(sdfs) == N
+        harr = (C.c_void_p * N)(*[s._h for s in sdfs])
+    lib().or_ik_coll_batch(mech._h, (sdf or sdfs[0])._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt),
+                           tgt.shape[1], C.byref(prm), _p(cp), sph.size, _p(sph) if sph.size else None,
+                           _p(r) if sph.size else None, C.cast(harr, C.c_void_p) if harr is not None else None,
                            _p(it), _p(err), n_threads)
     return q, it, err
+
+
+def ikc_sphere_order(tree: UrdfTree, q_joint_ids, link_id, sphere_links):
+    """The order in which kin_ik_coll_batch adds the sphere rows (kinhip_host.cpp stage_ikc_tree): spheres on
+    the root frame first, then by the depth-first position (children in joint order) of the moving joint
+    whose frame carries them, the caller's order inside a carrier."""
+    J = len(tree.joint_names)
+    cols = {}
+    for c, j in enumerate(q_joint_ids):
+        cols[int(j)] = c  # a repeated joint keeps its last column
+    moving = {j for j in cols if tree.joint_type[j - 1] != FIXED}
+    pjoint = {int(tree.joint_clink[j - 1]): j for j in range(1, J + 1)}
+    needed = set()
+
+    def mark(l):
+        while l is not None and l not in needed:
+            needed.add(l)
+            pj = pjoint.get(l)
+            l = int(tree.joint_plink[pj - 1]) if pj else None
+
+    mark(int(link_id))
+    for l in sphere_links:
+        mark(int(l))
+    children = {}
+    for j in range(1, J + 1):
+        children.setdefault(int(tree.joint_plink[j - 1]), []).append(j)
+    carrier = {}
+    count = [0]
+
+    def visit(x, car):
+        carrier[x] = car
+        for j in children.get(x, []):
+            c = int(tree.joint_clink[j - 1])
+            if c not in needed:
+                continue
+            if j in moving:
+                s = count[0]
+                count[0] += 1
+                visit(c, s)
+            else:
+                visit(c, car)
+
+    for l in range(1, len(tree.link_names) + 1):
+        if l in needed and l not in pjoint:
+            visit(l, -1)
+    return sorted(range(len(sphere_links)), key=lambda k: (carrier[int(sphere_links[k])], k))
 
 
 def rot_error(T_target, T_now):

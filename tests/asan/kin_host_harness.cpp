@@ -78,6 +78,12 @@ void exercise_model(kin_model* m, int with_base) {
         const int rc = kin_coll_plan_create(m, &c, &cp);
         check_rc(rc, "coll_plan_create");
         if (rc == KIN_OK) kin_plan_destroy(cp);
+        // collision-aware IK plan: the tree of this link and the spheres (host staging runs before any
+        // device allocation)
+        kin_plan* ip = nullptr;
+        const int rc2 = kin_coll_ik_plan_create(m, &c, (int32_t)(rnd() % (nl + 2)), &ip);
+        check_rc(rc2, "coll_ik_plan_create");
+        if (rc2 == KIN_OK) kin_plan_destroy(ip);
     }
     (void)with_base;
 }

@@ -16,8 +16,8 @@ hipError_t launch_ik_dls(const KProg<T>&, const KStep<T>*, const LaunchGeom&, co
     return hipErrorNoDevice;
 }
 template <typename T>
-hipError_t launch_ik_coll(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, const LaunchGeom&,
-                          const CollArgs&, const IkcArgs&, const IkArgs&, const T*, int64_t, const T*, T*, int64_t,
+hipError_t launch_ik_tree(const KIkcProg<T>&, const KIkcStep<T>*, const KSphere<T>*, const KBox<T>*, const CollArgs&,
+                          const SceneLaunch*, const IkcArgs&, const IkArgs&, const T*, int64_t, const T*, T*, int64_t,
                           int64_t, int32_t*, T*, int64_t, const JitFns*, hipStream_t) {
     return hipErrorNoDevice;
 }
@@ -50,8 +50,8 @@ hipError_t launch_pose_residual(const T*, int64_t, const T*, int64_t, int64_t, i
     template hipError_t launch_ik_dls<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const IkArgs&,        \
                                          const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t,  \
                                          const JitFns*, const IkScratch&, hipStream_t);                              \
-    template hipError_t launch_ik_coll<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,      \
-                                          const LaunchGeom&, const CollArgs&, const IkcArgs&, const IkArgs&,         \
+    template hipError_t launch_ik_tree<T>(const KIkcProg<T>&, const KIkcStep<T>*, const KSphere<T>*, const KBox<T>*, \
+                                          const CollArgs&, const SceneLaunch*, const IkcArgs&, const IkArgs&,        \
                                           const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t,   \
                                           const JitFns*, hipStream_t);                                               \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*, int64_t, \

@@ -85,3 +85,20 @@ def test_two_rank_shards_match_single_process():
     ref, _ = O.OracleMech(tree).fk_jac_batch(Qfull, ids, tree.link_id("gripper_link"), ids)
     np.testing.assert_array_equal(allp, ref)
     assert split0 == (0, 501) and split == (501, 500)
+
+
+def test_local_rank_beyond_the_gpus_is_refused(monkeypatch):
+    """One process per GPU: LOCAL_RANK >= the visible GPU count raises instead of silently
+    putting two ranks on one GPU; only the explicit gloo rehearsal may share a GPU."""
+    import kinhip.dist as D
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.delenv("KINHIP_DIST_BACKEND", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    with pytest.raises(RuntimeError, match="one process per GPU"):
+        D.init_from_env()
+    picked = []
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: picked.append(d))
+    ctx = D.init_from_env(backend="gloo")  # rehearsal: ranks share GPU 0
+    assert ctx.device == torch.device("cuda", 0) and picked == [torch.device("cuda", 0)]

@@ -116,13 +116,15 @@ def _oracle_scene(sdf):
     import oracle as O
     tree = O.parse_urdf_tree(golden("fetch.urdf"))
     om = O.OracleMech(tree)
-    sph, rad = [], []
+    sph, rad, par = [], [], []
     for name, c, r in kinhip.FETCH_ARM_SPHERES:
         T = np.eye(4)
         T[:3, 3] = c
         sph.append(om.add_new_link(tree.link_id(name), T))
         rad.append(r)
+        par.append(tree.link_id(name))
     box = O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+    _oracle_scene.parents = par
     return O, tree, om, sph, rad, box
 
 
@@ -219,12 +221,14 @@ def test_batched_collision_ik_pillar(target, link, size, dtype):
     assert float((D1 < 0.02).float().mean()) > 0.4
 
 
-@pytest.mark.parametrize("spec", [False, True])
-def test_collision_ik_iterates_vs_oracle(spec):
+@pytest.mark.parametrize("spec,lanes", [(False, 0), (False, 4), (True, 0), (True, 1), (True, 4), (True, 16),
+                                        (True, 64)])
+def test_collision_ik_iterates_vs_oracle(spec, lanes):
     """kin_ik_coll_batch (fp64) vs its CPU restatement (oracle or_ik_coll_batch): from the same seeds
     (the GPU's stage-1 solutions of 512 fridge targets) the same iteration counts, angles within 1e-7,
-    errors and minimum sphere distances within 1e-9 -- generic and plan-specialised kernels, the
-    reference's rpy objective with restarts."""
+    errors and minimum sphere distances within 1e-9 -- generic and plan-specialised kernels, every lane
+    layout (restarts = 2: 3 attempts, so a 4-group layout idles one group from the start),
+    the reference's rpy objective with restarts."""
     import oracle as O
     m, arm, sscc, sdf = _scene()
     gl = m.find_link("gripper_link")
@@ -244,10 +248,11 @@ def test_collision_ik_iterates_vs_oracle(spec):
     plan.ik_dls(tgt, Q1, Q0=Q0, max_iters=64, restarts=3, seed=2, with_rot=2)  # stage 1 (seeds for both)
     kw = dict(margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=96, lam=1e-2, tol_pos=1e-4, tol_rot=1e-4,
               max_step=0.5, with_rot=2, restarts=2, seed=7)
-    Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, **kw)
+    Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, **kw)
     O_, tree, om, sph, rad, box = _oracle_scene(sdf)
     ids = [tree.joint_id(n) for n in ARM]
-    rq, rit, rerr = O.ik_coll_batch(om, box, Q1.cpu().numpy(), ids, tree.link_id("gripper_link"), tg, sph, rad, **kw)
+    rq, rit, rerr = O.ik_coll_batch(om, box, Q1.cpu().numpy(), ids, tree.link_id("gripper_link"), tg, sph, rad,
+                                    sphere_parents=_oracle_scene.parents, **kw)
     it = it.cpu().numpy()
     assert (it <= 96).mean() > 0.8
     np.testing.assert_array_equal(it, rit)
@@ -258,11 +263,12 @@ def test_collision_ik_iterates_vs_oracle(spec):
 @pytest.mark.parametrize("spec", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_collision_ik_lanes_identical(spec, dtype):
-    """kin_ik_coll_batch runs the restart attempts of a target side by side on 4 lanes (specialised
-    kernels, >= 4 attempts, auto for small batches) or in sequence on one lane (lanes = 1): every lane's
-    arithmetic is the sequential schedule's, so angles, iteration counts and errors are bit-identical --
-    out of place and in place, with 4 attempts (one per lane) and 5 (lane 0 runs attempts 0 and 4);
-    the generic kernels (one lane per target whatever `lanes` says) give the same answers."""
+    """kin_ik_coll_batch runs the restart attempts of a target side by side in 4 lane groups and shares its
+    spheres out over 16 lanes per group (specialised kernels; auto for small batches, or forced: lanes = 4,
+    16, 64) or runs everything in sequence on one lane (lanes = 1): the sphere rows enter the normal
+    equations in the same order, so angles, iteration counts and errors are bit-identical -- out of place
+    and in place, with 4 attempts (one per group) and 5 (group 0 runs attempts 0 and 4); the generic
+    kernels (one lane per target whatever `lanes` says) give the same answers."""
     m, arm, sscc, sdf = _scene()
     gl = m.find_link("gripper_link")
     dev = torch.device("cuda", 0)
@@ -283,7 +289,7 @@ def test_collision_ik_lanes_identical(spec, dtype):
         kw = dict(margin=0.02, band=0.01, max_iters=max_iters, tol_pos=1e-4, tol_rot=1e-4, with_rot=2,
                   restarts=restarts, seed=7)
         ref = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=1, **kw)
-        for lanes in (0, 4):
+        for lanes in (0, 4, 16, 64):
             got = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, **kw)
             for a, b in zip(got, ref):
                 assert torch.equal(a, b), (restarts, lanes)

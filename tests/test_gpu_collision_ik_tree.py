@@ -1,0 +1,291 @@
+"""Collision-aware IK on the reference's scene shapes (/root/reference/fridge_demo.jl:13-37,
+test/test_inverse_kinematics.jl:52-86): spheres on more than one moving chain, a planar base, and a union
+attached to a scene mechanism with its joint values per target.  fp64 kin_ik_coll_batch(_scene) vs the CPU
+restatement (oracle or_ik_coll_batch, the sphere rows in the kernel's order): equal iteration counts, angles
+within 1e-7, |dp| / |rot| / min distance within 1e-9, generic and plan-specialised kernels.  The reference's
+own scene (PR2, both arms, 14 joints + base) needs the network-downloaded PR2 model; these scenes have the
+same structure (two arms off one torso, a base, an articulated fridge).  Sphere placement is
+parity-unpinned (no meshes)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import ARM, golden
+
+import kinhip
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=96, lam=1e-2, tol_pos=1e-4, tol_rot=1e-4,
+          max_step=0.5, with_rot=2, restarts=2, seed=7)
+
+# two arms of four revolute joints off a prismatic torso (the PR2 / fridge_demo.jl structure, smaller)
+TWO_ARM = """<robot name="twoarm">
+  <link name="base_link"/><link name="torso"/>
+  <link name="l1"/><link name="l2"/><link name="l3"/><link name="l4"/><link name="l_grip"/>
+  <link name="r1"/><link name="r2"/><link name="r3"/><link name="r4"/><link name="r_grip"/>
+  <joint name="torso_joint" type="prismatic"><parent link="base_link"/><child link="torso"/>
+    <origin xyz="0 0 0.8"/><axis xyz="0 0 1"/><limit lower="0" upper="0.3" effort="1" velocity="1"/></joint>
+  <joint name="l_j1" type="revolute"><parent link="torso"/><child link="l1"/><origin xyz="0.05 0.2 0.2"/>
+    <axis xyz="0 0 1"/><limit lower="-2" upper="2" effort="1" velocity="1"/></joint>
+  <joint name="l_j2" type="revolute"><parent link="l1"/><child link="l2"/><origin xyz="0.1 0 0"/>
+    <axis xyz="0 1 0"/><limit lower="-1.5" upper="1.5" effort="1" velocity="1"/></joint>
+  <joint name="l_j3" type="continuous"><parent link="l2"/><child link="l3"/><origin xyz="0.3 0 0"/>
+    <axis xyz="1 0 0"/></joint>
+  <joint name="l_j4" type="revolute"><parent link="l3"/><child link="l4"/><origin xyz="0.05 0 0"/>
+    <axis xyz="0 1 0"/><limit lower="-2.2" upper="2.2" effort="1" velocity="1"/></joint>
+  <joint name="l_tool" type="fixed"><parent link="l4"/><child link="l_grip"/><origin xyz="0.3 0 0"/></joint>
+  <joint name="r_j1" type="revolute"><parent link="torso"/><child link="r1"/><origin xyz="0.05 -0.2 0.2"/>
+    <axis xyz="0 0 1"/><limit lower="-2" upper="2" effort="1" velocity="1"/></joint>
+  <joint name="r_j2" type="revolute"><parent link="r1"/><child link="r2"/><origin xyz="0.1 0 0"/>
+    <axis xyz="0 1 0"/><limit lower="-1.5" upper="1.5" effort="1" velocity="1"/></joint>
+  <joint name="r_j3" type="continuous"><parent link="r2"/><child link="r3"/><origin xyz="0.3 0 0"/>
+    <axis xyz="1 0 0"/></joint>
+  <joint name="r_j4" type="revolute"><parent link="r3"/><child link="r4"/><origin xyz="0.05 0 0"/>
+    <axis xyz="0 1 0"/><limit lower="-2.2" upper="2.2" effort="1" velocity="1"/></joint>
+  <joint name="r_tool" type="fixed"><parent link="r4"/><child link="r_grip"/><origin xyz="0.3 0 0"/></joint>
+</robot>
+"""
+TWO_ARM_Q = ["r_j1", "r_j2", "r_j3", "r_j4", "torso_joint", "l_j1", "l_j2", "l_j3", "l_j4"]
+TWO_ARM_SPHERES = [(side + n, c, r) for side in ("l", "r") for n, c, r in
+                   (("2", (0.1, 0, 0), 0.05), ("2", (0.22, 0, 0), 0.05), ("4", (0.1, 0, 0), 0.045),
+                    ("4", (0.25, 0, 0), 0.04))]
+
+
+def _pose(t, yaw=0.0):
+    T = np.eye(4)
+    c, s = np.cos(yaw), np.sin(yaw)
+    T[:3, :3] = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+    T[:3, 3] = t
+    return T
+
+
+def _col(T):
+    return np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+
+
+class Scene:
+    """The robot on the GPU side and the oracle's restatement, the same spheres on both."""
+
+    def __init__(self, urdf_path, q_names, spheres, with_base=False):
+        import oracle as O
+        self.O = O
+        self.m = kinhip.parse_urdf(urdf_path, with_base=with_base)
+        self.q = [self.m.find_joint(n) for n in q_names]
+        self.sscc = kinhip.SweptSphereCollisionChecker(self.m)
+        self.tree = O.parse_urdf_tree(urdf_path)
+        self.om = O.OracleMech(self.tree, with_base=with_base)
+        self.sph, self.rad, self.par = [], [], []
+        for name, c, r in spheres:
+            self.sscc.add_coll_sphere(self.m.find_link(name), c, r)
+            T = np.eye(4)
+            T[:3, 3] = c
+            self.sph.append(self.om.add_new_link(self.tree.link_id(name), T))
+            self.rad.append(r)
+            self.par.append(self.tree.link_id(name))
+        self.ids = [self.tree.joint_id(n) for n in q_names]
+        self.nd = len(q_names) + (3 if with_base else 0)
+
+    def sphere_centres(self, q, link_names):
+        """World centres of the spheres at configuration q (oracle FK)."""
+        self.om.set_joint_angles(self.ids, q)
+        return [self.om.get_transform(s)[:3, 3] for s in self.sph]
+
+    def check(self, link, tg, Q1, sdf, box=None, boxes=None, spec=False, lanes=0, scene_q=None, kw=KW,
+              min_conv=0.5):
+        plan = kinhip.CollisionIKPlan(self.sscc, self.m.find_link(link), self.q, dtype=torch.float64)
+        if spec:
+            plan.specialize()
+        dev = Q1.device
+        tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+        Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, scene_q=scene_q, **kw)
+        rq, rit, rerr = self.O.ik_coll_batch(self.om, box, Q1.cpu().numpy(), self.ids, self.tree.link_id(link), tg,
+                                             self.sph, self.rad, sdfs=boxes, sphere_parents=self.par, **kw)
+        it = it.cpu().numpy()
+        conv = it <= kw["max_iters"]
+        assert conv.mean() >= min_conv, conv.mean()
+        np.testing.assert_array_equal(it, rit)
+        np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+        np.testing.assert_allclose(err.cpu().numpy(), rerr, atol=1e-9)
+        return Q, it, err
+
+
+def _fridge_box():
+    import oracle as O
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    sdf = kinhip.fridge_sdf(fr)
+    return sdf, O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+
+
+def _fridge_targets(rng, N):
+    tg = np.zeros((12, N))
+    for k in range(N):
+        tg[:, k] = _col(_pose((rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32)),
+                              rng.uniform(-0.3, 0.3)))
+    return tg
+
+
+def _stage1(sc, link, tg, dev):
+    """Stage-1 solutions (collision-free DLS on the same plan) as the stage-2 seeds."""
+    plan = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link(link), sc.q, dtype=torch.float64)
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    Q1 = torch.zeros((sc.nd, tg.shape[1]), dtype=torch.float64, device=dev)
+    plan.ik_dls(tgt, Q1, max_iters=64, restarts=3, seed=2, with_rot=2)  # (in place: other columns stay 0)
+    return Q1
+
+
+@pytest.mark.parametrize("spec,lanes", [(False, 0), (True, 0), (True, 1), (True, 64)])
+def test_fetch_arm_with_head_spheres(spec, lanes):
+    """Spheres on two moving chains of Fetch: the arm (torso .. wrist) and the head (head_pan, head_tilt are
+    q columns too: they move no target, only head spheres -- the solver moves them out of a box placed on
+    the head of the stage-1 solution).  The tree branches at torso_lift_link (a saved branch frame)."""
+    import oracle as O
+    names = ARM + ["head_pan_joint", "head_tilt_joint"]
+    spheres = kinhip.FETCH_ARM_SPHERES + [("head_pan_link", (0.1, 0.0, 0.1), 0.1),
+                                          ("head_tilt_link", (0.05, 0.0, 0.0), 0.09),
+                                          ("head_tilt_link", (0.15, 0.0, 0.0), 0.06)]
+    sc = Scene(golden("fetch.urdf"), names, spheres)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(41)
+    N = 256
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev)
+    # a box on the head of target 0's stage-1 solution: every target's head starts in collision
+    c = sc.sphere_centres(Q1[:, 0].cpu().numpy(), None)[-2]
+    sdf0, _ = _fridge_box()
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(_pose(c + [0.0, 0.0, 0.05]), (0.12, 0.3, 0.12))])
+    box = O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+    Q, it, err = sc.check("gripper_link", tg, Q1, sdf, box=box, spec=spec, lanes=lanes)
+    # the head joints moved (they only move head spheres)
+    moved = np.abs(Q.cpu().numpy()[8:10] - Q1.cpu().numpy()[8:10]).max(axis=0)
+    assert (moved[it <= KW["max_iters"]] > 1e-3).mean() > 0.5
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("spec,lanes", [(False, 0), (True, 0), (True, 16)])
+def test_two_arm_tree(tmp_path, spec, lanes, with_base):
+    """Two arms off one torso (fridge_demo.jl's joints = vcat(rarm, larm) with spheres on both arms): the
+    target is the left gripper, the right arm's joints move only right-arm spheres.  A box sits on the
+    right forearm of the stage-1 solutions, so the solve must move the right arm while the left holds its
+    pose.  With a planar base: 9 joints + 3 base columns = 12 variables."""
+    import oracle as O
+    path = tmp_path / "twoarm.urdf"
+    path.write_text(TWO_ARM)
+    sc = Scene(str(path), TWO_ARM_Q, TWO_ARM_SPHERES, with_base=with_base)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(43)
+    N = 300
+    tg = np.zeros((12, N))
+    for k in range(N):
+        tg[:, k] = _col(_pose((rng.uniform(0.35, 0.55), rng.uniform(0.15, 0.35), rng.uniform(0.95, 1.2)),
+                              rng.uniform(-0.4, 0.4)))
+    Q1 = _stage1(sc, "l_grip", tg, dev)
+    Q1[:4] = torch.tensor([0.3, 0.4, 0.0, 0.6], dtype=torch.float64, device=dev)[:, None]  # right arm start
+    c = sc.sphere_centres(Q1[:, 0].cpu().numpy(), None)[6]  # r4's first sphere
+    sdf = kinhip.UnionSDF([kinhip.BoxSDF(_pose(c), (0.1, 0.1, 0.1)),
+                           kinhip.BoxSDF(_pose((0.6, 0.0, 0.4)), (0.8, 1.2, 0.05))])
+    box = O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+    Q, it, err = sc.check("l_grip", tg, Q1, sdf, box=box, spec=spec, lanes=lanes)
+    conv = it <= KW["max_iters"]
+    moved = np.abs(Q.cpu().numpy()[:4] - Q1.cpu().numpy()[:4]).max(axis=0)
+    assert (moved[conv] > 1e-3).mean() > 0.5  # the right arm left the box
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_fetch_with_base_in_fridge(spec):
+    """Fetch with its planar base (8 joints + x, y, theta): stage 2 in the fridge scene of
+    test/test_inverse_kinematics.jl:52-86, the base a variable of every sphere row."""
+    sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES, with_base=True)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(47)
+    N = 256
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev)
+    sdf, box = _fridge_box()
+    sc.check("gripper_link", tg, Q1, sdf, box=box, spec=spec)
+
+
+def test_door_angle_per_target():
+    """fridge_demo.jl's scene with the door angle a per-target input (kin_ik_coll_batch_scene: the fridge
+    as a UnionSDF attached to its mechanism, scene columns door + base per target) vs the oracle's static
+    union of each target's fridge state (oracle.fridge_boxes)."""
+    import oracle as O
+    sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(53)
+    N = 192
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev)
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    doors = rng.uniform(1.5, 2.4, N)
+    scene_q = torch.tensor(np.stack([doors, np.full(N, 1.2), np.zeros(N), np.zeros(N)]), dtype=torch.float64,
+                           device=dev).contiguous()
+    ft = O.parse_urdf_tree(golden("fridge.urdf"))
+    boxes = [O.OracleUnionSDF(*O.fridge_boxes(ft, door_angle=d, base=(1.2, 0.0, 0.0))) for d in doors]
+    sc.check("gripper_link", tg, Q1, asdf, box=None, boxes=boxes, scene_q=scene_q)
+    # one scene state for the whole batch == the static union of that state
+    plan = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link("gripper_link"), sc.q, dtype=torch.float64)
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    a = plan.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q[:, 0].contiguous(), **KW)
+    fr2 = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    b = plan.ik_coll(kinhip.fridge_sdf(fr2, door_angle=float(doors[0])), tgt, torch.empty_like(Q1), Q0=Q1, **KW)
+    # (the attached union places its boxes by FK on the device, the static one on the host: last-bit
+    # differences, so the iteration counts may split on a handful of targets)
+    ia, ib = a[1].cpu().numpy(), b[1].cpu().numpy()
+    same = ia == ib
+    assert same.mean() > 0.98
+    np.testing.assert_allclose(a[0].cpu().numpy()[:, same], b[0].cpu().numpy()[:, same], atol=1e-7)
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_unsolvable_targets_return_the_best_attempt(spec):
+    """a target no attempt can solve (inside a box: the pose and the constraint conflict)
+    returns the attempt whose end state has the lowest merit |dp|^2 + |rot|^2 + w^2 max(0, margin - d)^2,
+    as NLopt returns its best point -- not the last re-drawn attempt.  Same rule in the oracle; the
+    returned err rows are the returned state's."""
+    import oracle as O
+    sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(59)
+    N = 128
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev)
+    sdf0, _ = _fridge_box()
+    # a box around the target region: the gripper's spheres cannot reach the targets without entering it
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(_pose((0.98, 0.0, 1.235)), (0.4, 0.4, 0.25))])
+    box = O.OracleUnionSDF([b.pose for b in sdf.sdfs], [b.width for b in sdf.sdfs])
+    Q, it, err = sc.check("gripper_link", tg, Q1, sdf, box=box, spec=spec, min_conv=0.0)
+    fail = it > KW["max_iters"]
+    assert fail.mean() > 0.5
+    # err of a failed target is the returned state's: recompute with the oracle
+    q = Q.cpu().numpy()
+    gl = sc.tree.link_id("gripper_link")
+    pose = sc.om.fk_batch(q, sc.ids, [gl])[0]
+    dp = np.linalg.norm(pose[9:] - tg[9:], axis=0)
+    np.testing.assert_allclose(dp[fail], err.cpu().numpy()[0][fail], atol=1e-9)
+    d, _ = O.coll_batch(sc.om, box, q, sc.ids, sc.sph, sc.rad, with_grad=False)
+    np.testing.assert_allclose(d.min(0)[fail], err.cpu().numpy()[2][fail], atol=1e-9)
+
+
+def test_padded_ldq_beyond_the_narrow_bound():
+    """the collision-aware IK with a leading dimension whose row offsets pass 2^31 bytes (fp64,
+    8 columns, ld = 2^25 + 64) -- every load and store of the kernel is 64-bit safe; the answers equal
+    those of a dense call."""
+    sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(61)
+    N = 256
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev)
+    sdf, _ = _fridge_box()
+    plan = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link("gripper_link"), sc.q, dtype=torch.float64).specialize()
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    ref = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, **KW)
+    ld = (1 << 25) + 64
+    big0 = torch.zeros((8, ld), dtype=torch.float64, device=dev)
+    big = torch.zeros((8, ld), dtype=torch.float64, device=dev)
+    big0[:, :N] = Q1
+    got = plan.ik_coll(sdf, tgt, big[:, :N], Q0=big0[:, :N], **KW)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2])
+    del big, big0
