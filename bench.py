@@ -243,14 +243,8 @@ def _coll_leg(ctx, stream, n, steps, spec=1, pad=256):
     Qtraj = (qs[:, :, None] + (qg - qs)[:, :, None] * tt).reshape(8, nt * 64).to(dt).to(ctx.device).contiguous()
     ns = plan.n_sph
     nbytes = 8 * 4 + ns * 4 + ns * 8 * 4
-    tile = 8192
-    Qt_rand, Qt_traj = kinhip.tiled(Q, tile), kinhip.tiled(Qtraj, tile)
     for name, Qx, run in (("ineq_const_random", Q, lambda: ic.eval_batch(Q, stream=stream)),
-                          ("ineq_const_trajectories", Qtraj, lambda: ic.eval_batch(Qtraj, stream=stream)),
-                          ("ineq_const_trajectories_tiled", Qtraj,
-                           lambda: ic.eval_batch_tiled(Qt_traj, n, stream=stream)),
-                          ("dists_grads_tiled", Q, lambda: plan.run_tiled(sdf, Qt_rand, n, grads=True,
-                                                                          stream=stream))):
+                          ("ineq_const_trajectories", Qtraj, lambda: ic.eval_batch(Qtraj, stream=stream))):
         with torch.cuda.stream(stream):
             for _ in range(3):
                 run()
@@ -273,15 +267,11 @@ def _coll_leg(ctx, stream, n, steps, spec=1, pad=256):
                      "achieved_GBs": (36 if name.startswith("min_dist") else nbytes) * nx / (dev_s / steps) / 1e9}
         if name.startswith("ineq"):
             out[name]["margin"] = 0.03
-        if name.endswith("tiled"):
-            out[name]["layout"] = f"tiled SoA, tile {tile}"
-    # ceilings of the distances + gradients legs (8 rows in, 14 + 112 rows out) from the same run
-    for name, tl_ in (("dists_grads", 0), ("dists_grads_tiled", tile)):
-        pat_c = _pattern_us(8, ns + ns * 8, n, tl_, stream, ld=0 if tl_ else ld)
-        out[name]["pattern_ceiling_us"] = pat_c
-        out[name]["frac_of_pattern"] = pat_c / out[name]["avg_launch_us"]
-        out[name]["frac"] = out[name]["achieved_GBs"] / HBM_PEAK_GBS
-    out["tiled_vs_plain_dists_grads"] = out["dists_grads"]["avg_launch_us"] / out["dists_grads_tiled"]["avg_launch_us"]
+    # ceiling of the distances + gradients leg (8 rows in, 14 + 112 rows out) from the same run
+    pat_c = _pattern_us(8, ns + ns * 8, n, 0, stream, ld=ld)
+    out["dists_grads"]["pattern_ceiling_us"] = pat_c
+    out["dists_grads"]["frac_of_pattern"] = pat_c / out["dists_grads"]["avg_launch_us"]
+    out["dists_grads"]["frac"] = out["dists_grads"]["achieved_GBs"] / HBM_PEAK_GBS
     out["workload"] = (f"fetch arm 8 joints, {plan.n_sph} spheres, fridge scene 7 boxes, {n} configs/GPU, f32, "
                        f"samples sharded across ranks, {'specialised' if spec else 'generic'} kernels")
     return out
@@ -364,7 +354,59 @@ def _scene_and_coll_ik_legs(ctx, stream, n, steps, spec=1):
                               "converged": float(conv.float().mean()),
                               "min_sphere_distance_converged": float(err[2][conv].min()) if bool(conv.any()) else None,
                               "kernels": "specialised" if spec else "generic"}
+    # the two stages apart: stage 2 alone from stage 1's answers (kin_ik_coll_batch)
+    kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2, index_base=ctx.rank * nt)
+    Q1 = torch.empty_like(Q0)
+    cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
+    Q2 = torch.empty_like(Q0)
+    _, dev2, _ = _timed_calls(ctx, stream, lambda: cplan.ik_coll(sdf, tg, Q2, Q0=Q1, margin=0.02, stream=stream, **kw),
+                              reps, warmup=1)
+    out["f3_collision_ik"]["ms_stage2"] = dev2 / reps * 1e3
+    out["f3_collision_ik"]["ms_stage1"] = out["f3_collision_ik"]["ms_per_batch"] - dev2 / reps * 1e3
+    for n_p in (4096, 65536):
+        out[f"f3_collision_ik_pillar_{n_p}"] = _pillar_leg(ctx, stream, m, arm, sscc, sdf, n_p, spec)
     return out
+
+
+def _pillar_leg(ctx, stream, m, arm, sscc, sdf0, nt, spec, reps=5):
+    """Stage 2 where it works: tests/test_gpu_collision_ik.py's pillar scene -- a box
+    (8 cm) on elbow_flex_link of the collision-free solution for the target (0.75, 0.15, 1.0), targets
+    jittered by +-5 mm, so stage 1's answers collide for most of them -- `nt` targets per GPU, fp32;
+    stage 1 once (kin_ik_dls_batch_from), then stage 2 (kin_ik_coll_batch) timed: stage-2 solves/s."""
+    dt = torch.float32
+    gl = m.find_link("gripper_link")
+    T0 = np.eye(4)
+    T0[:3, 3] = (0.75, 0.15, 1.0)
+    m.set_joint_angles(arm, np.zeros(8))
+    kinhip.inverse_kinematics_(m, gl, arm, T0)
+    P = np.eye(4)
+    P[:3, 3] = kinhip.get_transform(m, m.find_link("elbow_flex_link"))[:3, 3]
+    m.set_joint_angles(arm, np.zeros(8))
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(P, (0.08, 0.08, 0.08))])
+    rng = np.random.default_rng(5 + ctx.rank)
+    tg = np.zeros((12, nt))
+    for k in range(nt):
+        t = np.asarray(T0[:3, 3]) + rng.uniform(-0.005, 0.005, 3)
+        tg[:, k] = np.concatenate([np.eye(3).reshape(-1), t])
+    tg = torch.tensor(tg, dtype=dt, device=ctx.device).contiguous()
+    cplan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dt)
+    if spec:
+        _specialize(cplan)
+    kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2, index_base=ctx.rank * nt)
+    Q0 = torch.zeros((8, nt), dtype=dt, device=ctx.device)
+    Q1 = torch.empty_like(Q0)
+    cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
+    _, _, D1 = sscc.plan(arm, dtype=dt).run(sdf, Q1, dists=False, min_dist=True)
+    Q2 = torch.empty_like(Q0)
+    wall, dev_s, (Q2, it, err) = _timed_calls(
+        ctx, stream, lambda: cplan.ik_coll(sdf, tg, Q2, Q0=Q1, margin=0.02, stream=stream, **kw), reps, warmup=1)
+    conv = it <= 128
+    return {"value": nt * ctx.world * reps / wall, "unit": "stage-2 solves/s (kin_ik_coll_batch)",
+            "targets_per_gpu": nt, "ms_per_batch": dev_s / reps * 1e3,
+            "stage1_answers_under_margin": float((D1 < 0.02).float().mean()),
+            "converged": float(conv.float().mean()),
+            "min_sphere_distance_converged": float(err[2][conv].min()) if bool(conv.any()) else None,
+            "kernels": "specialised" if spec else "generic"}
 
 
 def _nakamura_leg(m, arm, gl, ctx, stream, n=1 << 18, reps=5, spec=1):
@@ -772,7 +814,6 @@ def main():
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec, pad=args.row_pad)
         out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("pmc_coll32s.json")
         out["config5_fk_sdf"]["dists_grads"]["pmc"] = _pmc_valu("pmc_collg32s.json")
-        out["config5_fk_sdf"]["dists_grads_tiled"]["pmc"] = _pmc_valu("pmc_collg32ts.json")
         out.update(_scene_and_coll_ik_legs(ctx, stream, N, max(5, args.steps // 2), spec=args.spec))
         out["a11_nakamura_f64"] = _nakamura_leg(m, arm, gl, ctx, stream, spec=args.spec)
         if args.spec:  # the same legs on the generic kernels (A/B of kin_plan_specialize)

@@ -345,6 +345,9 @@ KINHIP_API int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* des
 KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q, int64_t ldq,
                               int64_t n, void* dists, int64_t ldd, void* grads, int64_t ldg, void* min_dist,
                               void* stream);
+/* (Layout: rows whose leading dimension is a power of two of >= 2^16 elements -- e.g. ld = n = 2^20 -- put a
+ * wave's 126 row streams on the same HBM channels; ld = n + 256 runs ~10% faster.  A tiled collision
+ * layout was measured and dropped: it lost to padded rows in two driver runs) */
 
 /* kin_coll_batch against boxes attached to a scene (kin_sdf_create_attached): scene_q [n_scene_cols][lds]
  * holds the scene joint values (+ base x, y, theta) of every sample -- one launch sweeps e.g. many door
@@ -354,13 +357,6 @@ KINHIP_API int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, doubl
                                     int64_t ldq, const void* scene_q, int64_t lds, int64_t n, void* dists,
                                     int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream);
 
-/* kin_coll_batch on the tiled layout (see kin_plan_run_tiled): element (config i,
- * row r) of q / dists / grads / min_dist at X[(i / tile) * ts + r * ld + i % tile]
- * (min_dist has one row; its ld is 1 element per configuration, ts its tile stride). */
-KINHIP_API int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double truncation, int64_t tile,
-                                    const void* q, int64_t ldq, int64_t tsq, int64_t n, void* dists, int64_t ldd,
-                                    int64_t tsd, void* grads, int64_t ldg, int64_t tsg, void* min_dist, int64_t tsm,
-                                    void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Collision-aware IK: inverse_kinematics!(m, link, joints, target, sscc, sdf;  */
@@ -424,10 +420,6 @@ KINHIP_API int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, co
 KINHIP_API int kin_ineq_const_batch(const kin_plan* coll_plan, const kin_sdf* sdf, double margin, const void* q,
                                     int64_t ldq, int64_t n, void* vals, int64_t ldv, void* jac, int64_t ldj,
                                     void* stream);
-/* kin_ineq_const_batch on the tiled layout (kin_coll_batch_tiled's conventions). */
-KINHIP_API int kin_ineq_const_batch_tiled(const kin_plan* coll_plan, const kin_sdf* sdf, double margin, int64_t tile,
-                                          const void* q, int64_t ldq, int64_t tsq, int64_t n, void* vals, int64_t ldv,
-                                          int64_t tsv, void* jac, int64_t ldj, int64_t tsj, void* stream);
 /* PoseConstraint (src/planning.jl:114-138) of one link for N configurations.
  * `p` must come from kin_plan_create with n_out = 1, jac_link = that link and
  * jac_flags = KIN_RPY_JAC | KIN_WITH_ROT (6 rows) or 0 (position only, 3 rows).

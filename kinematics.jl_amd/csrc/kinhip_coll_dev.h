@@ -181,7 +181,7 @@ struct SceneArgs {
 };
 template <typename T, int MAXG>
 struct SceneCtx {
-    const KSceneGroup* groups;
+    KSceneGroup gr[MAXG];  // the groups' descriptors, loaded once (uniform: scalar registers)
     int ng;
     T inv[MAXG][12];  // per lane: world -> group frame (row-major 3x4); MAXG >= ng (register budget)
 };
@@ -200,13 +200,13 @@ __device__ __forceinline__ void axis_rotation(const T* __restrict__ u, T th, T (
 // the group frames of this sample (get_transform(scene, link) up to the group's moving frame), inverted
 template <typename T, int MAXG>
 __device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG>& sc, const SceneArgs<T>& sa, uint32_t off) {
-    sc.groups = sa.groups;
     sc.ng = sa.ng;
     const uint32_t so = sa.uniform ? 0u : off;
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
         if (g >= sa.ng) break;  // uniform
-        const KSceneGroup& G = sa.groups[g];
+        sc.gr[g] = sa.groups[g];
+        const KSceneGroup& G = sc.gr[g];
         Fr<T> f;
         if (sa.base_col >= 0)
             base_frame(f, ld_soa(sa.q, sa.base_col, sa.ld, so), ld_soa(sa.q, sa.base_col + 1, sa.ld, so),
@@ -259,15 +259,29 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const K
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
         if (g >= sc.ng) break;  // uniform
-        const KSceneGroup& G = sc.groups[g];
+        const KSceneGroup& G = sc.gr[g];
         const T* I = sc.inv[g];
         T lx[NS], ly[NS], lz[NS], dg[NS], gg[NS][3];
+        // Exact cull: every box of the group lies in its enclosing box (bc, bh), so the distance to that
+        // box is a lower bound of the group's distance; a group that cannot come below the minimum of the
+        // earlier groups (dg < d takes a group) is skipped -- with a slack beyond the rounding of both
+        // distances, so the skip never changes a result.  (The door of fridge_demo.jl's scene is a small
+        // group: most spheres skip it.)
+        bool need = false;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             lx[i] = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
             ly[i] = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
             lz[i] = fma(I[8], px[i], fma(I[9], py[i], fma(I[10], pz[i], I[11])));
+            const T ox = fmax(fabs(lx[i] - (T)G.bc[0]) - (T)G.bh[0], T(0));
+            const T oy = fmax(fabs(ly[i] - (T)G.bc[1]) - (T)G.bh[1], T(0));
+            const T oz = fmax(fabs(lz[i] - (T)G.bc[2]) - (T)G.bh[2], T(0));
+            const T lb2 = fma(ox, ox, fma(oy, oy, oz * oz));
+            // d + slack (d = +inf: never culled; d < 0: only a point clearly outside the group's box)
+            const T lim = fmax(d[i] + fma(fabs(d[i]), T(1e-4), T(1e-5)), T(1e-5));
+            need |= !(lb2 > lim * lim);
         }
+        if (!need) continue;  // (per lane: a wave skips the group when none of its lanes needs it)
         union_sdf<T, GRAD, NS>(boxes + G.box0, aabb + G.aabb0, G.na, G.nb, lx, ly, lz, dg, gg,
                                smem + (size_t)G.box0 * sizeof(KBox<T>), use_lds);
 #pragma unroll

@@ -1326,6 +1326,21 @@ int kin_sdf_create_attached(const kin_model* scene, int32_t n_q, const int32_t* 
         for (int32_t k = 0; k < n_boxes; ++k)
             if (bs[k].group == (int32_t)g && !aa[k]) mem.push_back(k);
         groups[g].nb = (int32_t)mem.size();
+        {  // the group frame's box enclosing its boxes (|R| h around t), rounded outward to float
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int32_t k : mem)
+                for (int i = 0; i < 3; ++i) {
+                    double e = 0;
+                    for (int j = 0; j < 3; ++j) e += fabs(bs[k].pose.r[3 * i + j]) * 0.5 * widths3[3 * k + j];
+                    lo[i] = std::min(lo[i], bs[k].pose.t[i] - e);
+                    hi[i] = std::max(hi[i], bs[k].pose.t[i] + e);
+                }
+            for (int i = 0; i < 3; ++i) {
+                const double c = 0.5 * (lo[i] + hi[i]), h = 0.5 * (hi[i] - lo[i]);
+                groups[g].bc[i] = (float)c;
+                groups[g].bh[i] = (float)(h + 1e-6 * (fabs(c) + h) + 1e-6);
+            }
+        }
         for (size_t o = 0; o < mem.size(); ++o) {
             const int32_t k = mem[o];
             const M34 inv = m_rigid_inverse(bs[k].pose);
@@ -1890,32 +1905,13 @@ int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncatio
     return KIN_OK;
 }
 
-int kin_coll_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double truncation, int64_t tile, const void* q,
-                         int64_t ldq, int64_t tsq, int64_t n, void* dists, int64_t ldd, int64_t tsd, void* grads,
-                         int64_t ldg, int64_t tsg, void* min_dist, int64_t tsm, void* stream) {
-    const TileArgs ta{tile, tsq, tsd, tsg, tsm};
-    const int ndof = p ? p->nqcols : 0;
-    int rc = coll_check(p, sdf, q, ldq, tsq, n, dists, ldd, tsd, p ? p->n_sph : 0, grads, ldg, tsg,
-                        p ? p->n_sph * ndof : 0, ta, "kin_coll_batch_tiled");
-    if (rc == KIN_OK && min_dist && tile < n && tsm < tile) rc = set_error(KIN_E_INVALID, "kin_coll_batch_tiled: tsm < tile");
-    if (rc != KIN_OK || n == 0) return rc;
-    return coll_launch(p, sdf, coll_args(sdf, truncation, 0.0), q, ldq, n, dists, ldd, grads, ldg, min_dist, ta,
-                       stream);
-}
-
 int kin_ineq_const_batch(const kin_plan* p, const kin_sdf* sdf, double margin, const void* q, int64_t ldq, int64_t n,
                          void* vals, int64_t ldv, void* jac, int64_t ldj, void* stream) {
-    return kin_ineq_const_batch_tiled(p, sdf, margin, n > 0 ? n : 1, q, ldq, 0, n, vals, ldv, 0, jac, ldj, 0, stream);
-}
-
-int kin_ineq_const_batch_tiled(const kin_plan* p, const kin_sdf* sdf, double margin, int64_t tile, const void* q,
-                               int64_t ldq, int64_t tsq, int64_t n, void* vals, int64_t ldv, int64_t tsv, void* jac,
-                               int64_t ldj, int64_t tsj, void* stream) {
     if (!std::isfinite(margin)) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: margin must be finite");
     if (!vals) return set_error(KIN_E_INVALID, "kin_ineq_const_batch: null vals");
-    const TileArgs ta = tile >= n ? plain_soa(n) : TileArgs{tile, tsq, tsv, tsj, 0};
+    const TileArgs ta = plain_soa(n > 0 ? n : 1);
     const int ndof = p ? p->nqcols : 0;
-    const int rc = coll_check(p, sdf, q, ldq, tsq, n, vals, ldv, tsv, p ? p->n_sph : 0, jac, ldj, tsj,
+    const int rc = coll_check(p, sdf, q, ldq, 0, n, vals, ldv, 0, p ? p->n_sph : 0, jac, ldj, 0,
                               p ? p->n_sph * ndof : 0, ta, "kin_ineq_const_batch");
     if (rc != KIN_OK || n == 0) return rc;
     // src/planning.jl:56, :66: truncation_dist = margin + 0.05; val = dist - margin

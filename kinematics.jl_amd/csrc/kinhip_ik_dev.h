@@ -16,6 +16,17 @@ namespace {
 #ifndef KINHIP_IK_FAST_ATAN
 #define KINHIP_IK_FAST_ATAN 1  // fp32: polynomial atan2 for the rotation error's angle (rot_error)
 #endif
+// fp32: the damped solve (J W J^T + lambda^2 I, its Cholesky, the two triangular solves and dq = J^T y)
+// in fp64 from the fp32 Jacobian.  Forming J J^T in fp32 errs by ~eps |J|^2 = 2.4e-7 against
+// lambda^2 = 1e-4, and at a singular arm (Fetch at q = 0: rank 4) y carries ~e / lambda^2 in the null
+// directions that J^T y cancels: an fp32 solve moves dq by up to 2e-3 rad against the fp64 oracle's,
+// the J rounding alone by 1e-6 (tools/ik_fp32_solve_error.py).  0: the fp32 solve (A/B build).
+#ifndef KINHIP_IK_F64SOLVE
+#define KINHIP_IK_F64SOLVE 1
+#endif
+// Contraction only inside one expression (a * b + c): the specialised kernels (hiprtc) fold constants
+// into the instruction stream, and fusing across statements would then differ from the generic ones
+#pragma clang fp contract(on)
 // Diagnostic section stamps (tools only: KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=<k> in the A/B build): the
 // cycles of iteration section k (1 FK, 2 errors + checks, 3 Jacobian + J W J^T, 4 Cholesky + solves,
 // 5 dq + active set, 6 step, 7 loop top) summed over the lane's iterations replace err row 0 and the
@@ -135,6 +146,15 @@ __device__ __forceinline__ void rot_error(const T (&Rt)[9], const T (&R)[9], T (
         for (int k = 0; k < 3; ++k) w[k] = a[k] / nn * th;
     }
 }
+
+template <bool F32>
+struct ik_solve_type {
+    using type = double;
+};
+template <>
+struct ik_solve_type<true> {
+    using type = float;
+};
 
 template <typename T>
 struct IkArgsT {
@@ -513,17 +533,19 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
 
         KIN_IK_STAMP(2);
-        T Jb[3][ROWS];
+        // the damped solve's arithmetic type: fp64 (also in the fp32 kernel, KINHIP_IK_F64SOLVE)
+        using TS = typename ik_solve_type<sizeof(T) == 4 && !KINHIP_IK_F64SOLVE>::type;
+        TS Jb[3][ROWS];
         if (base) {
 #pragma unroll
             for (int k = 0; k < 3; ++k)
 #pragma unroll
-                for (int r = 0; r < ROWS; ++r) Jb[k][r] = T(0);
-            Jb[0][0] = T(1);
-            Jb[1][1] = T(1);
-            Jb[2][0] = -(Lf.t[1] - b[1]);
-            Jb[2][1] = Lf.t[0] - b[0];
-            if constexpr (ROWS == 6) Jb[2][5] = T(1);
+                for (int r = 0; r < ROWS; ++r) Jb[k][r] = TS(0);
+            Jb[0][0] = TS(1);
+            Jb[1][1] = TS(1);
+            Jb[2][0] = -(TS)(Lf.t[1] - b[1]);
+            Jb[2][1] = (TS)(Lf.t[0] - b[0]);
+            if constexpr (ROWS == 6) Jb[2][5] = TS(1);
         }
         // linear Jacobian rows z x (p - o) once per iteration (the solve and dq reuse them)
 #pragma unroll
@@ -555,15 +577,15 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         T mx = T(0);
         {
             // A = J W J^T + lambda^2 I  (lower triangle)
-            T A[ROWS][ROWS];
+            TS A[ROWS][ROWS];
 #pragma unroll
             for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? a.lam2 : T(0);
-            // fp32: entries (r, 2k) and (r, 2k + 1) in one packed FMA (v_pk_fma_f32, J[r] broadcast):
+                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? (TS)a.lam2 : TS(0);
+            // fp32 solve: entries (r, 2k) and (r, 2k + 1) in one packed FMA (v_pk_fma_f32, J[r] broadcast):
             // 12 instead of 21 per joint, each element the same fma (identical results).  One wave per
             // SIMD issues a packed FMA in ~1.5x the time of a scalar one (tools/pk_probe.hip).
-            constexpr bool pk = KINHIP_IK_PK && sizeof(T) == 4 && ROWS == 6;
+            constexpr bool pk = KINHIP_IK_PK && sizeof(TS) == 4 && ROWS == 6;
             typedef float f2 __attribute__((ext_vector_type(2)));
             f2 A2[pk ? ROWS : 1][pk ? ROWS / 2 : 1];
             if constexpr (pk) {
@@ -596,14 +618,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                     for (int r = 0; r < ROWS; ++r)
 #pragma unroll
                         for (int c = 0; c <= r; ++c)
-                            if (r < nr) A[r][c] = fma(J[r], J[c], A[r][c]);
+                            if (r < nr) A[r][c] = fma((TS)J[r], (TS)J[c], A[r][c]);
                 }
             }
             if constexpr (pk) {
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-                    for (int c = 0; c <= r; ++c) A[r][c] = (T)((c & 1) ? A2[r][c / 2].y : A2[r][c / 2].x);
+                    for (int c = 0; c <= r; ++c) A[r][c] = (TS)((c & 1) ? A2[r][c / 2].y : A2[r][c / 2].x);
             }
             if (base) {
 #pragma unroll
@@ -614,47 +636,55 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                         for (int c = 0; c <= r; ++c) A[r][c] = fma(Jb[k][r], Jb[k][c], A[r][c]);
             }
             KIN_IK_STAMP(3);
-            // Cholesky A = L L^T (in place, lower), then y = A^-1 e.  fp32 keeps the
-            // reciprocal square root of each pivot (hardware v_rsq_f32) and multiplies:
-            // the 6 square roots and 27 divisions of the IEEE form are ~10 instructions
-            // each and dominated the iteration.  fp64 keeps the oracle's exact form
-            // (its iterates are compared with or_ik_dls_batch to 1e-7).
+            // Cholesky A = L L^T (in place, lower), then y = A^-1 e.  The fp32 kernel keeps the
+            // reciprocal square root of each pivot and multiplies: the 6 square roots and 27 divisions
+            // of the IEEE form are ~10 instructions each and dominated the iteration -- v_rsq_f32 for an
+            // fp32 solve, v_rsq_f64 plus one Newton step (~2^-44) for its fp64 solve.  The fp64 kernel
+            // keeps the oracle's exact form (its iterates are compared with or_ik_dls_batch to 1e-7).
             constexpr bool fast = sizeof(T) == 4;
-            T ip[ROWS];  // 1 / L[j][j] (fp32)
+            auto rsq = [](TS d) -> TS {
+                if constexpr (sizeof(TS) == 4) {
+                    return rsqrt_fast(d);
+                } else {
+                    const double r = __builtin_amdgcn_rsq(d);
+                    return r * fma(-0.5 * d * r, r, 1.5);
+                }
+            };
+            TS ip[ROWS];  // 1 / L[j][j] (fp32 kernel)
 #pragma unroll
             for (int j = 0; j < ROWS; ++j) {
-                T d = A[j][j];
+                TS d = A[j][j];
 #pragma unroll
-                for (int k = 0; k < j; ++k) d -= A[j][k] * A[j][k];
+                for (int k = 0; k < j; ++k) d = fma(-A[j][k], A[j][k], d);
                 if constexpr (fast) {
-                    ip[j] = rsqrt_fast(d);
+                    ip[j] = rsq(d);
                 } else {
                     d = sqrt_t(d);
                     A[j][j] = d;
                 }
 #pragma unroll
                 for (int r = j + 1; r < ROWS; ++r) {
-                    T sm = A[r][j];
+                    TS sm = A[r][j];
 #pragma unroll
-                    for (int k = 0; k < j; ++k) sm -= A[r][k] * A[j][k];
+                    for (int k = 0; k < j; ++k) sm = fma(-A[r][k], A[j][k], sm);
                     if constexpr (fast) A[r][j] = sm * ip[j];
                     else A[r][j] = sm / d;
                 }
             }
-            T y[ROWS];
+            TS y[ROWS];
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
-                T sm = e[r];
+                TS sm = (TS)e[r];
 #pragma unroll
-                for (int k = 0; k < r; ++k) sm -= A[r][k] * y[k];
+                for (int k = 0; k < r; ++k) sm = fma(-A[r][k], y[k], sm);
                 if constexpr (fast) y[r] = sm * ip[r];
                 else y[r] = sm / A[r][r];
             }
 #pragma unroll
             for (int r = ROWS - 1; r >= 0; --r) {
-                T sm = y[r];
+                TS sm = y[r];
 #pragma unroll
-                for (int k = r + 1; k < ROWS; ++k) sm -= A[k][r] * y[k];
+                for (int k = r + 1; k < ROWS; ++k) sm = fma(-A[k][r], y[k], sm);
                 if constexpr (fast) y[r] = sm * ip[r];
                 else y[r] = sm / A[r][r];
             }
@@ -664,11 +694,12 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
                 jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
-                T v = T(0);
+                TS vs = TS(0);
                 const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;  // (zero angular rows)
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
-                    if (r < nr) v = fma(J[r], y[r], v);
+                    if (r < nr) vs = fma((TS)J[r], y[r], vs);
+                const T v = (T)vs;
                 const bool held = (blk >> s) & 1u;
                 dq[s] = held ? T(0) : v;
                 // pushed further out of a limit it sits on (selects, no short-circuit branches)
@@ -680,20 +711,20 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             if (base) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    T v = T(0);
+                    TS v = TS(0);
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r) v = fma(Jb[k][r], y[r], v);
-                    db[k] = v;
-                    mx = fmax(mx, fabs(v));
+                    db[k] = (T)v;
+                    mx = fmax(mx, fabs(db[k]));
                 }
             }
         }
         KIN_IK_STAMP(5);
         const T sc = mx > a.max_step ? a.max_step / mx : T(1);
 #pragma unroll
-        for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(qs[s] + sc * dq[s], S[s].lo), S[s].hi);
+        for (int s = 0; s < MAXA; ++s) qs[s] = fmin(fmax(fma(sc, dq[s], qs[s]), S[s].lo), S[s].hi);
         if (base)
-            for (int k = 0; k < 3; ++k) b[k] = b[k] + sc * db[k];
+            for (int k = 0; k < 3; ++k) b[k] = fma(sc, db[k], b[k]);
         ++it;
         KIN_IK_STAMP(6);
     }
@@ -758,3 +789,5 @@ __device__ __forceinline__ void nakamura_body(const KProg<T>& P, const KStep<T>*
 
 }  // namespace
 }  // namespace kinhip
+
+#pragma clang fp contract(fast)  // (the translation unit's default again: -ffp-contract=fast-honor-pragmas)

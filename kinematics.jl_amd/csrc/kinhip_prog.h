@@ -121,6 +121,9 @@ struct KSceneGroup {
     int32_t na, nb;        // axis-aligned boxes (first), all boxes
     int32_t aabb0;
     int32_t pad[2];
+    float bc[3], bh[3];    // the group frame's box enclosing all its boxes (rounded outward): a lower
+                           // bound of the group's distance (scene_union's exact cull)
+    int32_t pad2[2];
 };
 constexpr int kMaxSceneGroups = 4;  // moving frames carrying boxes (per-lane frames in registers)
 

@@ -36,8 +36,8 @@ EXPORTS = [
     "kin_plan_specialize", "kin_plan_specialized", "kin_jit_selfcheck",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
     "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_point_ik_nakamura_batch",
-    "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch", "kin_coll_batch_tiled",
-    "kin_ineq_const_batch", "kin_ineq_const_batch_tiled", "kin_pose_const_batch",
+    "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
+    "kin_ineq_const_batch", "kin_pose_const_batch",
     "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
     "kin_coll_batch_scene",
 ]
@@ -130,10 +130,6 @@ def lib():
         "kin_coll_plan_create": ([P, P, P], C.c_int),
         "kin_coll_batch": ([P, P, C.c_double, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
         "kin_ineq_const_batch": ([P, P, C.c_double, P, I64, I64, P, I64, P, I64, P], C.c_int),
-        "kin_coll_batch_tiled": ([P, P, C.c_double, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P, I64, P],
-                                 C.c_int),
-        "kin_ineq_const_batch_tiled": ([P, P, C.c_double, I64, P, I64, I64, I64, P, I64, I64, P, I64, I64, P],
-                                       C.c_int),
         "kin_pose_const_batch": ([P, P, I64, P, I64, I64, P, I64, P, I64, P, I64, P], C.c_int),
         "kin_coll_ik_plan_create": ([P, P, I32, P], C.c_int),
         "kin_sdf_create_attached": ([P, I32, P, I32, P, P, P, P], C.c_int),

@@ -157,27 +157,6 @@ class CollisionPlan:
         K.check(K.lib().kin_plan_specialized(self._h, C.byref(v)))
         return v.value
 
-    def run_tiled(self, sdf: UnionSDF, Qt: torch.Tensor, n: int, dists=True, grads=False, min_dist=False,
-                  truncation=float("inf"), stream=None):
-        """kin_coll_batch_tiled: Qt (ntiles, n_dof, tile) -> dists (ntiles, n_sph, tile), grads
-        (ntiles, n_sph, n_dof, tile), min_dist (ntiles, tile) (contiguous), n <= ntiles * tile.  Async."""
-        if Qt.dtype != self.dtype or not Qt.is_cuda or Qt.dim() != 3 or Qt.shape[1] != self.n_dof or \
-                not Qt.is_contiguous():
-            raise ValueError(f"Qt must be a contiguous CUDA {self.dtype} tensor of shape (ntiles, {self.n_dof}, tile)")
-        nt, _, tile = Qt.shape
-        _plan_device(self, Qt)
-        _plan_device(sdf, Qt)
-        dev = Qt.device
-        D = torch.empty((nt, self.n_sph, tile), dtype=self.dtype, device=dev) if dists else None
-        G = torch.empty((nt, self.n_sph, self.n_dof, tile), dtype=self.dtype, device=dev) if grads else None
-        Mn = torch.empty((nt, tile), dtype=self.dtype, device=dev) if min_dist else None
-        st = (stream or torch.cuda.current_stream(dev)).cuda_stream
-        ptr = lambda t: t.data_ptr() if t is not None else None
-        K.check(K.lib().kin_coll_batch_tiled(self._h, sdf._h, float(truncation), tile, Qt.data_ptr(), tile,
-                                             self.n_dof * tile, int(n), ptr(D), tile, self.n_sph * tile, ptr(G), tile,
-                                             self.n_sph * self.n_dof * tile, ptr(Mn), tile, st))
-        return D, G, Mn
-
     def run(self, sdf: UnionSDF, Q: torch.Tensor, dists=True, grads=False, min_dist=False,
             truncation=float("inf"), stream=None, scene_q: Optional[torch.Tensor] = None):
         """-> (dists [n_sph, N] | None, grads [n_sph, n_dof, N] | None, min_dist [N] | None). Async.

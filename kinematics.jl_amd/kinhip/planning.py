@@ -85,22 +85,6 @@ class IneqConst:
                                              V.data_ptr(), N, G.data_ptr() if G is not None else None, N, st))
         return V, G
 
-    def eval_batch_tiled(self, Qt: torch.Tensor, n: int, with_jac=True, stream=None):
-        """kin_ineq_const_batch_tiled: Qt (ntiles, n_dof, tile) -> vals (ntiles, n_coll, tile),
-        jac (ntiles, n_coll, n_dof, tile) or None.  Async."""
-        if Qt.dtype != self.dtype or not Qt.is_cuda or Qt.dim() != 3 or Qt.shape[1] != self.n_dof or \
-                not Qt.is_contiguous():
-            raise ValueError(f"Qt must be a contiguous CUDA {self.dtype} tensor of shape (ntiles, {self.n_dof}, tile)")
-        nt, _, tile = Qt.shape
-        V = torch.empty((nt, self.n_coll, tile), dtype=self.dtype, device=Qt.device)
-        G = torch.empty((nt, self.n_coll, self.n_dof, tile), dtype=self.dtype, device=Qt.device) if with_jac else None
-        st = (stream or torch.cuda.current_stream(Qt.device)).cuda_stream
-        K.check(K.lib().kin_ineq_const_batch_tiled(self.plan._h, self.sdf._h, self.margin, tile, Qt.data_ptr(), tile,
-                                                   self.n_dof * tile, int(n), V.data_ptr(), tile, self.n_coll * tile,
-                                                   G.data_ptr() if G is not None else None, tile,
-                                                   self.n_coll * self.n_dof * tile, st))
-        return V, G
-
     def __call__(self, xi, val_vec: np.ndarray, jac_mat: np.ndarray):
         xi = np.asarray(xi, np.float64)
         Q = torch.tensor(xi.reshape(self.n_wp, self.n_dof).T.copy(), dtype=self.dtype, device=_device())

@@ -448,9 +448,10 @@ def test_gpu_collision_broad_phase_exact(dtype, spec):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("spec", [False, True])
-def test_gpu_collision_tiled_layout(dtype, spec):
-    """kin_coll_batch_tiled / kin_ineq_const_batch_tiled == the plain layout, bit for bit (partial last
-    tile, one tile, multi-chain plan, min distance accumulated across chains)."""
+def test_gpu_collision_padded_rows(dtype, spec):
+    """Row-padded views (the bench's layout: ld = n + 256, the C-ABI's ldq / ldd / ldg) == dense rows, bit
+    for bit, for kin_coll_batch and kin_ineq_const_batch (multi-chain plan, min distance accumulated across
+    chains).  (The tiled collision layout was dropped: it lost to padded rows on the driver's boxes.)"""
     import kinhip
     dev = torch.device("cuda", 0)
     m, sscc, arm = _gpu_setup(False)
@@ -463,18 +464,15 @@ def test_gpu_collision_tiled_layout(dtype, spec):
     if spec:
         plan.specialize()
     g = torch.Generator().manual_seed(12)
-    for N, tile in ((3000, 256), (5000, 1024), (600, 1024)):
+    for N, pad in ((3000, 256), (5000, 64)):
         Q = (torch.rand((10, N), generator=g, dtype=torch.float64) * 3 - 1.5).to(dtype).to(dev)
         D0, G0, M0 = plan.run(sdf, Q, grads=True, min_dist=True, truncation=0.2)
-        Dt, Gt, Mt = plan.run_tiled(sdf, kinhip.tiled(Q, tile), N, grads=True, min_dist=True, truncation=0.2)
-        assert torch.equal(kinhip.untiled(Dt, N), D0) and torch.equal(kinhip.untiled(Gt, N), G0)
-        assert torch.equal(kinhip.untiled(Mt, N), M0)
-        ic = kinhip.IneqConst(sscc, joints, sdf, 1, 0.03, dtype=dtype)
-        if spec:
-            ic.plan.specialize()
-        V0, J0 = ic.eval_batch(Q)
-        Vt, Jt = ic.eval_batch_tiled(kinhip.tiled(Q, tile), N)
-        assert torch.equal(kinhip.untiled(Vt, N), V0) and torch.equal(kinhip.untiled(Jt, N), J0)
+        Qb = torch.zeros((10, N + pad), dtype=dtype, device=dev)
+        Qb[:, :N] = Q
+        Dp = torch.zeros((plan.n_sph, N + pad), dtype=dtype, device=dev)[:, :N]
+        Gp = torch.zeros((plan.n_sph, 10, N + pad), dtype=dtype, device=dev)[:, :, :N]
+        D1, G1, M1 = plan.run(sdf, Qb[:, :N], dists=Dp, grads=Gp, min_dist=True, truncation=0.2)
+        assert torch.equal(D1, D0) and torch.equal(G1, G0) and torch.equal(M1, M0)
 
 
 @pytest.mark.gpu

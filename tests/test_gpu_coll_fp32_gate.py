@@ -48,9 +48,15 @@ def test_coll_fp32_bench_path_at_the_north_star_bound():
     assert plan.specialized == kinhip.KIN_SPEC_COLL
     _, _, Mn = plan.run(sdf, Q, dists=False, min_dist=True)
     D, G, Mn2 = plan.run(sdf, Q, grads=True, min_dist=True)
-    Dt, Gt, _ = plan.run_tiled(sdf, kinhip.tiled(Q, 8192), n, grads=True)
+    # the bench's exact layout: rows padded to ld = n + 256 (bench.py _coll_leg), equal bit for bit
+    ld = n + 256
+    Qb = torch.zeros((8, ld), dtype=torch.float32, device=dev)
+    Qb[:, :n] = Q
+    Dp = torch.zeros((plan.n_sph, ld), dtype=torch.float32, device=dev)[:, :n]
+    Gp = torch.zeros((plan.n_sph, 8, ld), dtype=torch.float32, device=dev)[:, :, :n]
+    plan.run(sdf, Qb[:, :n], dists=Dp, grads=Gp)
     torch.cuda.synchronize()
-    assert torch.equal(kinhip.untiled(Dt, n), D) and torch.equal(kinhip.untiled(Gt, n), G)
+    assert torch.equal(Dp, D) and torch.equal(Gp, G)
     tree = O.parse_urdf_tree(golden("fetch.urdf"))
     om = O.OracleMech(tree)
     sph, rad = [], []

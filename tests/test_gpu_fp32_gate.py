@@ -109,3 +109,24 @@ def test_ground_truth_json_fp32_headline_kernel(dev, with_base):
         worst = max(worst, float(et.max()), float(er.max()))
     print(f"ground_truth.json through the fp32 headline kernel: max abs error {worst:.3e}")
     assert worst <= TOL32, worst
+
+
+def test_config2_bench_path_full_batch_vs_oracle(dev):
+    """config 2's exact bench path -- FK of the 6 exampel.jl:11 links in fp64, the
+    plan-specialised kernel on the tiled layout (tile 4096), the bench's 2^20 counter-hashed dataset --
+    every one of the 2^20 x 6 x 12 outputs against the fp64 oracle at 1e-9 (the fp64 gate)."""
+    from conftest import EXAMPLE_LINKS
+    m = kinhip.parse_urdf(golden("fetch.urdf"))
+    arm = [m.find_joint(n) for n in ARM]
+    links = [m.find_link(n) for n in EXAMPLE_LINKS]
+    N, tile = 1 << 20, 4096
+    Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, dtype=torch.float64,
+                               device=dev)
+    plan = m.plan(arm, out_links=links, dtype=torch.float64).specialize(kinhip.KIN_SPEC_FK)
+    Pt, _ = plan.run_tiled(kinhip.tiled(Q, tile), N)
+    got = kinhip.untiled(Pt, N).cpu().numpy()  # [6, 12, N]
+    om = O.OracleMech(O.parse_urdf_tree(golden("fetch.urdf")))
+    ref = om.fk_batch(Q.cpu().numpy(), [j.id for j in arm], [l.id for l in links])
+    e = float(np.abs(got - ref).max())
+    print(f"config 2 bench path vs oracle at 2^20: max|pose| {e:.3e}")
+    assert e <= 1e-9, e

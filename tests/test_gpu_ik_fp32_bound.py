@@ -2,13 +2,10 @@
 sits from the fp64 oracle restatement, on 4,096 Fetch targets from the bench's
 within-limit distribution.
 
-  * One damped step from the same seed: |q32 - q64| <= delta * |e0| / lambda^2 per target, with
-    delta = 1e-6 the fp32 FK / Jacobian accuracy the north star gates (tests/test_gpu_fp32_gate.py)
-    and |e0| the target's initial residual: dq = J^T (J J^T + lambda^2 I)^-1 e, and a perturbation
-    delta of J moves dq by at most ~delta |e| / lambda^2 (||(J J^T + lambda^2 I)^-1|| <= 1 / lambda^2).
-    Measured (tools/ik_fp32_vs_fp64.py): max 1.2e-3, p50 5.5e-5 against bounds of ~1e-2 -- the
-    damped solve amplifies the fp32 rounding of J by up to ~1/lambda^2, which is the problem's
-    conditioning, not the kernel's.
+  * One damped step from the same seed: |q32 - q64| <= 1e-4, and within the
+    perturbation bound delta * |e0| / lambda^2 (delta = 1e-6, the fp32 FK / J gate).  The fp32 kernel
+    solves J W J^T + lambda^2 I in fp64 (KINHIP_IK_F64SOLVE): forming it in fp32 errs by ~eps |J|^2 against
+    lambda^2 = 1e-4, which at Fetch's singular q = 0 moved dq by up to 2e-3 (round 3: 1.2e-3 measured).
   * Config-4 settings end to end: >= 99% of the targets converge in both precisions, >= 98% with
     equal iteration counts, and on those the answers agree to p99 5e-3 rad (measured 1.5e-3; a
     redundant 8-joint arm can end on a different point of the same target's solution set, so no
@@ -57,7 +54,11 @@ def test_one_step_within_the_perturbation_bound(setup):
     d = np.abs(Q.double().cpu().numpy() - rq).max(0)
     bound = 1e-6 * e0 / KW["lam"] ** 2
     assert np.all(d <= bound), float((d / bound).max())
-    assert np.median(d) < 2e-4
+    # the damped solve runs in fp64 from the fp32 Jacobian (KINHIP_IK_F64SOLVE): what is left is the fp32
+    # rounding of J itself (~1e-6 at q = 0, tools/ik_fp32_solve_error.py), not the 1/lambda^2 amplification
+    # of an fp32 J J^T (2e-3 before)
+    print(f"one fp32 step vs fp64: max {d.max():.2e}, p50 {np.median(d):.2e}")
+    assert d.max() <= 1e-4, float(d.max())
 
 
 def test_config4_answers_agree(setup):

@@ -20,12 +20,9 @@ cp = sscc.plan(arm, dtype=dt).specialize()
 n = 1 << 20
 Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=555, dtype=dt,
                            device=dev)
-TILE = int(os.environ.get("COLL_TILE", "8192"))
-Qt = kinhip.tiled(Q, TILE)
 res = []
 for name, run in (("min", lambda: cp.run(sdf, Q, dists=False, min_dist=True)),
-                  ("grad", lambda: cp.run(sdf, Q, dists=True, grads=True)),
-                  ("grad_tiled", lambda: cp.run_tiled(sdf, Qt, n, grads=True))):
+                  ("grad", lambda: cp.run(sdf, Q, dists=True, grads=True))):
     for _ in range(3):
         r = run()
     torch.cuda.synchronize()
@@ -38,4 +35,4 @@ for name, run in (("min", lambda: cp.run(sdf, Q, dists=False, min_dist=True)),
     us = e0.elapsed_time(e1) / 20 * 1e3
     chk = float(r[2].double().sum()) if name == "min" else float(r[1].double().abs().sum())
     res.append(f"{name}: {us:6.1f}us chk {chk:.9e}")
-print("tile", TILE, " | ".join(res), flush=True)
+print(" | ".join(res), flush=True)

@@ -11,7 +11,7 @@
 #   rccl                        the RCCL test + the bench under a one-rank RCCL group (KINHIP_DIST_ALWAYS_GROUP=1)
 #   pmc=<tag>:<workload>[,...]  per workload a kernel trace + stats, then separate --pmc passes (never with
 #                               trace domains; each pass within the per-block counter limits); workloads of
-#                               tools/prof_kernel.py (e.g. fkjac32ts, ik32s, coll32s, collg32s, collg32ts)
+#                               tools/prof_kernel.py (e.g. fkjac32ts, ik32s, coll32s, collg32s, cik32s)
 #   ik                          config-4 IK timing (product, twice) and 1M targets; per-iteration probe
 #   ik-sections                 iteration section stamps (A/B build, -DKINHIP_IK_SECT=k)
 #   ik-timeline                 per-lane entry / write timeline of one solve (A/B build)

@@ -108,6 +108,34 @@ elif a.what == "cik32":  # bench f3_collision_ik: stage 2 (kin_ik_coll_batch) of
     cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
     for _ in range(a.steps):
         cplan.ik_coll(sdf, tg, torch.empty_like(Q1), Q0=Q1, margin=0.02, **kw)
+elif a.what == "cikp32":  # bench f3_collision_ik_pillar_4096: stage 2 around a pillar on the elbow
+    import numpy as np
+    fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+    sdf0 = kinhip.fridge_sdf(fr)
+    sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+    T0 = np.eye(4)
+    T0[:3, 3] = (0.75, 0.15, 1.0)
+    m.set_joint_angles(arm, np.zeros(8))
+    kinhip.inverse_kinematics_(m, gl, arm, T0)
+    P = np.eye(4)
+    P[:3, 3] = kinhip.get_transform(m, m.find_link("elbow_flex_link"))[:3, 3]
+    m.set_joint_angles(arm, np.zeros(8))
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(P, (0.08, 0.08, 0.08))])
+    nt = 4096
+    rng = np.random.default_rng(5)
+    tg = np.zeros((12, nt))
+    for k in range(nt):
+        tg[:, k] = np.concatenate([np.eye(3).reshape(-1), T0[:3, 3] + rng.uniform(-0.005, 0.005, 3)])
+    tg = torch.tensor(tg, dtype=dt, device=dev).contiguous()
+    cplan = kinhip.CollisionIKPlan(sscc, gl, arm, dtype=dt)
+    if SPEC:
+        cplan.specialize()
+    Q0 = torch.zeros((8, nt), dtype=dt, device=dev)
+    Q1 = torch.empty_like(Q0)
+    kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2)
+    cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
+    for _ in range(a.steps):
+        cplan.ik_coll(sdf, tg, torch.empty_like(Q1), Q0=Q1, margin=0.02, **kw)
 elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge scene
     fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
     sdf = kinhip.fridge_sdf(fr)
@@ -116,11 +144,7 @@ elif a.what.startswith("coll"):  # config 5: Fetch arm spheres vs the fridge sce
     if SPEC:
         cp.specialize()
     grads = a.what.startswith("collg")
-    if a.what.endswith("t"):  # tiled layout (bench: dists_grads_tiled)
-        Qt = kinhip.tiled(Q, a.tile)
-        for _ in range(a.steps):
-            cp.run_tiled(sdf, Qt, a.n, dists=True, grads=True)
-    elif grads:  # rows padded like the bench's plain leg (ld = n + pad)
+    if grads:  # rows padded like the bench's plain leg (ld = n + pad)
         Qb = torch.empty((8, ld), dtype=dt, device=dev)
         Qb[:, :a.n] = Q
         Q = Qb[:, :a.n]

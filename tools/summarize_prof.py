@@ -49,10 +49,12 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "scene32s": ("kinhip_jit_colls_1_2_f32", ((8 + 4) + 14 + 14 * 8 + 1) * 4 * (1 << 20),
                  "f2 door sweep (bench f2_scene_door_sweep): boxes attached to the fridge, one door angle per sample, "
                  "14 distances + 14x8 gradients + the minimum, fp32, N = 2^20, specialised 2-group scene kernel"),
-    "cik32s": ("kinhip_jit_ikc_6_4_f32", 4096 * (12 + 8 + 8 + 1 + 3) * 4,
+    "cik32s": ("kinhip_jit_ikt_6_", 4096 * (12 + 8 + 8 + 1 + 3) * 4,
                "f3 stage 2 (bench f3_collision_ik): kin_ik_coll_batch of 4,096 fridge targets from stage 1's answers, "
-               "128 iterations, 3 restarts on 4 lanes per target, fp32, specialised (latency-bound: one target "
-               "runs every attempt)"),
+               "128 iterations, 3 restarts side by side in 4 lane groups of 16 sphere lanes, fp32, specialised"),
+    "cikp32s": ("kinhip_jit_ikt_6_", 4096 * (12 + 8 + 8 + 1 + 3) * 4,
+                "bench f3_collision_ik_pillar_4096: stage 2 of 4,096 targets around a pillar on the elbow (most "
+                "stage-1 answers collide), 128 iterations, 3 restarts, fp32, specialised"),
     "fkjac64": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20"),
     "fk6_64": ("k_fk<double, 8>", (8 + 72) * 8 * (1 << 20), "FK of 6 links (config 2), fp64, N = 2^20"),
     "ik32": ("k_ik_dls<float, 8, 6, 4>", 65536 * (12 + 8 + 8 + 1 + 2) * 4,
