@@ -138,6 +138,8 @@ def lib():
         "kin_ik_coll_batch_scene": ([P, P, P, P, P, I64, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("KINHIP_LIB") and not hasattr(L, name):
+            continue  # tools-only builds of older sources (tools/ikc_fault_probe.py) lack newer entries
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

@@ -1,0 +1,13 @@
+# round-4 session B: the whole GPU suite, smoke, the default bench, then the fault probe of the old
+# generic 4-lane kernel (last: it may fault the GPU)
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --maxfail=15 --timeout 300 --timeout-method thread \
+    > gpurun_out/r04b_tests.log 2>&1
+rc=$?
+grep -E "FAIL|ERROR|passed|failed" gpurun_out/r04b_tests.log | tail -30
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04b_smoke.log 2>&1 \
+  && tail -2 gpurun_out/r04b_smoke.log \
+  && timeout -k 10 600 python -u bench.py > gpurun_out/r04b_bench.json 2> gpurun_out/r04b_bench.err \
+  && tail -c 600 gpurun_out/r04b_bench.json \
+  && bash tools/ikc_fault_session.sh
