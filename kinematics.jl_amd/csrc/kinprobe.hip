@@ -1,41 +1,116 @@
 // kinprobe.hip -- measurement probe (not part of the engine's C-ABI): the HBM access pattern of a
 // kernel's inputs and outputs with no arithmetic, so bench.py can print each leg's ceiling from the
-// same run ("frac_of_pattern" = probe time / kernel time).  Element (config i, row r) of an array
-// lives at (i / tile) * rows * tile + r * tile + i % tile (tiled SoA, kin_plan_run_tiled) or at
-// r * ld + i (plain SoA, tile = 0); every lane reads rows_in rows of q and writes rows_out rows with
-// non-temporal stores, exactly like k_fk / k_coll.  Built into lib/libkinprobe.so by the Makefile.
+// same run ("frac_of_pattern" = probe time / kernel time).  The probe addresses memory exactly as the
+// kernels do (kinhip_device.h, kinhip_fk_dev.h): one buffer descriptor per row (ld_soa / st_soa; the
+// collision kernels' soffset form sto_soa for their outputs), a 32-bit lane byte offset, the tile of a
+// workgroup from a uniform 32-bit divide (Tiling::tile_blocks), 256-lane workgroups, non-temporal
+// stores, compile-time row counts, and -- for batches of 2^23 and more, like launch_fk's specialised
+// kernel -- the grid-strided form with the next unit's loads issued before this unit's stores.
+// Element (config i, row r) lives at (i / tile) * rows * tile + r * tile + i % tile (tiled SoA,
+// kin_plan_run_tiled) or at r * ld + i (plain SoA, tile = 0).  Built into lib/libkinprobe.so.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
+#include "kinhip_device.h"
+
+namespace kinhip {
 namespace {
 
-__global__ __launch_bounds__(256) void p_pattern(const float* __restrict__ q, float* __restrict__ out, int64_t n,
-                                                 int rows_in, int rows_out, int64_t tile, int64_t ldq, int64_t ldo) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t t = tile > 0 ? i / tile : 0, e = tile > 0 ? i % tile : i;
-    const float* qt = q + t * rows_in * ldq + e;
-    float* ot = out + t * rows_out * ldo + e;
+template <int RI>
+__device__ __forceinline__ float probe_load(const float* __restrict__ q, int64_t ldq, uint32_t off) {
+    float v[RI];
+#pragma unroll
+    for (int r = 0; r < RI; ++r) v[r] = ld_soa(q, r, ldq, off);
     float a = 0.0f;
-    for (int r = 0; r < rows_in; ++r) a += qt[r * ldq];
-    for (int r = 0; r < rows_out; ++r) __builtin_nontemporal_store(a + (float)r, ot + (int64_t)r * ldo);
+#pragma unroll
+    for (int r = 0; r < RI; ++r) a += v[r];
+    return a;
 }
 
-}  // namespace
+template <int RO, bool SOFF>
+__device__ __forceinline__ void probe_store(float* __restrict__ out, int64_t ldo, uint32_t off, float a) {
+#pragma unroll
+    for (int r = 0; r < RO; ++r) {
+        if constexpr (SOFF) sto_soa(out, r, ldo, off, a + (float)r);
+        else st_soa(out, r, ldo, off, a + (float)r);
+    }
+}
 
-// plain rows (tile = 0) ld elements apart (ld >= n: a padded row stride); tiled: ld is the tile
-extern "C" __attribute__((visibility("default"))) int kinprobe_pattern_ld(int rows_in, int rows_out, int64_t n,
-                                                                          int64_t tile, int64_t ld, const float* q,
-                                                                          float* out, void* stream) {
-    if (n <= 0 || rows_in < 0 || rows_out < 1 || tile < 0 || (tile > 0 ? ld != tile : ld < n)) return -1;
-    hipLaunchKernelGGL(p_pattern, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, q, out, n,
-                       rows_in, rows_out, tile, ld, ld);
+// one configuration per lane (k_fk / k_coll at batches below 2^23)
+template <int RI, int RO, bool SOFF>
+__global__ __launch_bounds__(256) void p_pattern(const float* __restrict__ q, int64_t ldq, float* __restrict__ out,
+                                                 int64_t ldo, int64_t n, Tiling tl) {
+    const uint32_t b = blockIdx.x, tid = threadIdx.x;
+    if ((uint64_t)b * 256u + tid >= (uint64_t)n) return;
+    const uint32_t t = b / tl.tile_blocks;
+    q += (int64_t)t * tl.tsq;
+    out += (int64_t)t * tl.tsp;
+    const uint32_t off = ((b - t * tl.tile_blocks) * 256u + tid) * 4u;
+    probe_store<RO, SOFF>(out, ldo, off, probe_load<RI>(q, ldq, off));
+}
+
+// grid-strided units of 256 configurations, the next unit's loads in flight (fk_body<..., true>)
+template <int RI, int RO, bool SOFF>
+__global__ __launch_bounds__(256) void p_pattern_strided(const float* __restrict__ q, int64_t ldq,
+                                                         float* __restrict__ out, int64_t ldo, int64_t n, Tiling tl) {
+    const uint32_t tid = threadIdx.x, units = (uint32_t)((n + 255) / 256);
+    uint32_t b = blockIdx.x;
+    if (b >= units) return;
+    auto addr = [&](uint32_t u, const float*& qb, float*& ob) {
+        const uint32_t t = u / tl.tile_blocks;
+        qb = q + (int64_t)t * tl.tsq;
+        ob = out + (int64_t)t * tl.tsp;
+        return ((u - t * tl.tile_blocks) * 256u + tid) * 4u;
+    };
+    const float* qb;
+    float* ob;
+    uint32_t off = addr(b, qb, ob);
+    float a = (uint64_t)b * 256u + tid < (uint64_t)n ? probe_load<RI>(qb, ldq, off) : 0.0f;
+    for (;;) {
+        const uint32_t bn = b + gridDim.x;
+        const bool more = bn < units;
+        const float* qn;
+        float* on;
+        const uint32_t offn = more ? addr(bn, qn, on) : 0u;
+        const float an = more && (uint64_t)bn * 256u + tid < (uint64_t)n ? probe_load<RI>(qn, ldq, offn) : 0.0f;
+        if ((uint64_t)b * 256u + tid < (uint64_t)n) probe_store<RO, SOFF>(ob, ldo, off, a);
+        if (!more) break;
+        b = bn; off = offn; ob = on; a = an;
+    }
+}
+
+template <int RI, int RO, bool SOFF>
+int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, hipStream_t st) {
+    const bool tiled = tile > 0;
+    if (tiled && tile % 256) return -1;
+    // tiled arrays: (ntiles, rows, tile) -- a tile of q is RI rows, a tile of out RO rows
+    Tiling tl{tiled ? (uint32_t)(tile / 256) : 0xffffffffu, tiled ? RI * tile : 0, tiled ? RO * tile : 0, 0, 0};
+    const int64_t ldr = tiled ? tile : ld;
+    if ((uint64_t)(tiled ? tile : n) * 4u >= (1ull << 31)) return -1;  // 32-bit lane offsets
+    if (SOFF && (uint64_t)(RO * ldr + (tiled ? tile : n)) * 4u >= (1ull << 31)) return -1;
+    const unsigned units = (unsigned)((n + 255) / 256);
+    if (per_lane > 1)
+        hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(256), 0, st,
+                           q, ldr, out, ldr, n, tl);
+    else
+        hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(256), 0, st, q, ldr, out, ldr, n, tl);
     return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
-extern "C" __attribute__((visibility("default"))) int kinprobe_pattern(int rows_in, int rows_out, int64_t n,
-                                                                       int64_t tile, const float* q, float* out,
-                                                                       void* stream) {
-    return kinprobe_pattern_ld(rows_in, rows_out, n, tile, tile > 0 ? tile : n, q, out, stream);
+}  // namespace
+}  // namespace kinhip
+
+// rows_in / rows_out: (8, 60) FK + 6x8 J + pose (k_fk), (8, 126) 14 sphere distances + gradients
+// (k_coll, soffset-addressed outputs).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
+// per_lane > 1: the grid-strided form with that many units per workgroup.
+extern "C" __attribute__((visibility("default"))) int kinprobe_pattern2(int rows_in, int rows_out, int64_t n,
+                                                                        int64_t tile, int64_t ld, int per_lane,
+                                                                        const float* q, float* out, void* stream) {
+    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1)
+        return -1;
+    const hipStream_t st = (hipStream_t)stream;
+    if (rows_in == 8 && rows_out == 60) return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, st);
+    if (rows_in == 8 && rows_out == 126) return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, st);
+    return -2;
 }

@@ -24,7 +24,7 @@ n = 1 << 20
 Q0 = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=555, dtype=dt,
                             device=dev)
 P = C.CDLL(os.path.join(ROOT, "kinematics.jl_amd", "lib", "libkinprobe.so"))
-P.kinprobe_pattern_ld.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+P.kinprobe_pattern2.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p]
 st = torch.cuda.current_stream(dev)
 
@@ -58,7 +58,7 @@ for rep in range(2):
         same = torch.equal(D, ref[0]) and torch.equal(G, ref[1])
         pq = torch.zeros(8 * ld, dtype=dt, device=dev)
         po = torch.zeros(126 * ld, dtype=dt, device=dev)
-        t_p = timed(lambda: P.kinprobe_pattern_ld(8, 126, n, 0, ld, pq.data_ptr(), po.data_ptr(), st.cuda_stream))
+        t_p = timed(lambda: P.kinprobe_pattern2(8, 126, n, 0, ld, 1, pq.data_ptr(), po.data_ptr(), st.cuda_stream))
         print(f"rep {rep} pad {pad:5d}: dists+grads {t_g:6.1f} us  pattern {t_p:6.1f} us  frac_of_pattern "
               f"{t_p / t_g:.3f}  min_dist {t_m:5.1f} us  identical {same}", flush=True)
         del Qb, Q, D, G, pq, po

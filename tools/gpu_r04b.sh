@@ -10,4 +10,5 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
   && tail -2 gpurun_out/r04b_smoke.log \
   && timeout -k 10 600 python -u bench.py > gpurun_out/r04b_bench.json 2> gpurun_out/r04b_bench.err \
   && tail -c 600 gpurun_out/r04b_bench.json \
+  && timeout -k 10 300 python -u tools/layout_probe.py > gpurun_out/r04b_layout.txt 2>&1 && cat gpurun_out/r04b_layout.txt \
   && bash tools/ikc_fault_session.sh
