@@ -271,6 +271,10 @@ typedef struct kin_ik_params {
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */
+    double damp_err;    /* error-scaled damping (Levenberg-Marquardt after Sugihara): each iteration solves with
+                           lambda^2 + damp_err * (|dp|^2 + |rot|^2) in place of lambda^2 -- heavy damping far from
+                           the target, lambda near it.  0: fixed lambda.  kin_ik_dls_batch(_from) only (the
+                           collision-aware IK requires 0).  Config 4's bench runs 0.01 (tools/ik_damp_explore.py) */
 } kin_ik_params;
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,

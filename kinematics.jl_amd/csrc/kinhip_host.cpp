@@ -1743,13 +1743,14 @@ int ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* pr
     if (prm->max_iters < 0 || !(prm->lambda > 0) || !(prm->max_step > 0) || prm->restarts < 0 ||
         prm->with_rot < 0 || prm->with_rot > 2 || prm->index_base < 0)
         return bad(KIN_E_INVALID, "bad IK parameters (lambda must be > 0)");
+    if (prm->damp_err != 0.0) return bad(KIN_E_INVALID, "kin_ik_params.damp_err must be 0 for the collision-aware IK");
     if (!std::isfinite(cp->margin) || !(cp->band >= 0) || !(cp->weight > 0) || !(cp->feas >= 0))
         return bad(KIN_E_INVALID, "bad collision parameters");
     if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8 &&
         prm->lanes != 16 && prm->lanes != 64)
         return bad(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4, 8, 16 or 64");
     const IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-                   prm->restarts, prm->seed, prm->lanes, prm->index_base};
+                   prm->restarts, prm->seed, prm->lanes, prm->index_base, 0.0};
     const IkcArgs c{cp->margin, cp->band, cp->weight, cp->feas};
     const CollArgs ca{INFINITY, 0.0, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
                       {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};
@@ -1957,8 +1958,10 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
     if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8)
         return set_error(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4 or 8");
     if (prm->index_base < 0) return set_error(KIN_E_INVALID, "kin_ik_params.index_base < 0");
+    if (!(prm->damp_err >= 0) || !std::isfinite(prm->damp_err))
+        return set_error(KIN_E_INVALID, "kin_ik_params.damp_err must be finite and >= 0");
     IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-             prm->restarts, prm->seed, prm->lanes, prm->index_base};
+             prm->restarts, prm->seed, prm->lanes, prm->index_base, prm->damp_err};
     // the specialised IK kernels address rows with 32-bit offsets (ldn_soa): every lane offset of a
     // launch chunk plus rows * ld must stay below 2^31 bytes, else the generic kernel runs
     const int64_t esz = p->dtype == KIN_F32 ? 4 : 8;

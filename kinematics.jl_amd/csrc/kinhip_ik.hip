@@ -122,6 +122,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     g_ik_partial = false;
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
                   0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
+    at.damp_err = T(a.damp_err);
     const int G = ik_group(n, natt, a.lanes);
     const int cus = ik_cus();
     const int64_t resident_waves = ik_resident_waves();

@@ -197,7 +197,16 @@ struct IkArgsT {
     int32_t p1_cut;
     int32_t cont;
     int32_t* fail_aux;
+    // error-scaled damping (kin_ik_params.damp_err): the solve's lambda^2 + damp_err (|dp|^2 + |rot|^2)
+    T damp_err;
 };
+
+// lambda^2 + mu (ep^2 + er^2) rounded operation by operation, as the oracle forms it (no contraction)
+template <typename S>
+__device__ __forceinline__ S ik_damping(S lam2, S mu, S ep, S er) {
+#pragma clang fp contract(off)
+    return lam2 + mu * (ep * ep + er * er);
+}
 
 // restart re-seed draw in [0, 1): identical to the oracle's or_ik_seed_u01
 __device__ __forceinline__ double ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col) {
@@ -578,10 +587,13 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         {
             // A = J W J^T + lambda^2 I  (lower triangle)
             TS A[ROWS][ROWS];
+            // (damp_err is uniform: a fixed-lambda call runs no extra instructions)
+            const TS lam2 = a.damp_err != T(0) ? ik_damping<TS>((TS)a.lam2, (TS)a.damp_err, (TS)ep, (TS)er)
+                                               : (TS)a.lam2;
 #pragma unroll
             for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? (TS)a.lam2 : TS(0);
+                for (int c = 0; c < ROWS; ++c) A[r][c] = (r == c) ? lam2 : TS(0);
             // fp32 solve: entries (r, 2k) and (r, 2k + 1) in one packed FMA (v_pk_fma_f32, J[r] broadcast):
             // 12 instead of 21 per joint, each element the same fma (identical results).  One wave per
             // SIMD issues a packed FMA in ~1.5x the time of a scalar one (tools/pk_probe.hip).

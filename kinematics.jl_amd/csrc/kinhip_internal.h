@@ -78,6 +78,7 @@ struct IkArgs {
     uint64_t seed;
     int32_t lanes;  // 0 auto
     int64_t index_base;  // global index of target 0 (restart draws)
+    double damp_err;     // error-scaled damping (k_ik_dls only)
 };
 
 // Device scratch of the two-phase IK schedule (launch_ik_dls): the list of targets attempt 0 did

@@ -67,6 +67,7 @@ struct KinIkParams
     seed::UInt64
     lanes::Int32
     index_base::Int64
+    damp_err::Float64
 end
 
 function check(rc::Cint)
@@ -264,14 +265,14 @@ Returns (Q, iters, err); converged where iters <= max_iters (max_iters + 1: no a
 function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
                                         Q::ROCMatrix{T}; max_iters=64, lambda=1e-2, tol_pos=1e-3, tol_rot=1e-3,
                                         max_step=0.5, with_rot=true, rpy_objective=false, restarts=0, seed=0, lanes=0,
-                                        index_base=0) where {T}
+                                        index_base=0, damp_err=0.0) where {T}
     N = size(Q, 1)
     ids = Int32[j.id for j in joints]
     p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
     iters = ROCVector{Int32}(undef, N)
     err = ROCMatrix{T}(undef, N, 2)
     mode = with_rot ? (rpy_objective ? 2 : 1) : 0
-    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, mode, restarts, seed, lanes, index_base)
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, mode, restarts, seed, lanes, index_base, damp_err)
     check(ccall((:kin_ik_dls_batch, libkinhip), Cint,
                 (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64,
                  Ptr{Cvoid}),
@@ -285,14 +286,15 @@ copyto!(Q, Q0) followed by inverse_kinematics!, without the copy (kin_ik_dls_bat
 function inverse_kinematics_from!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
                                   Q0::ROCMatrix{T}, Q::ROCMatrix{T}; max_iters=64, lambda=1e-2, tol_pos=1e-3,
                                   tol_rot=1e-3, max_step=0.5, with_rot=true, restarts=0, seed=0, lanes=0,
-                                  index_base=0) where {T}
+                                  index_base=0, damp_err=0.0) where {T}
     N = size(Q, 1)
     size(Q0) == size(Q) && stride(Q0, 2) == stride(Q, 2) || throw(DimensionMismatch("Q0 and Q differ in shape"))
     ids = Int32[j.id for j in joints]
     p = plan!(hm, T, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
     iters = ROCVector{Int32}(undef, N)
     err = ROCMatrix{T}(undef, N, 2)
-    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, with_rot, restarts, seed, lanes, index_base)
+    prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, with_rot, restarts, seed, lanes, index_base,
+                      damp_err)
     check(ccall((:kin_ik_dls_batch_from, libkinhip), Cint,
                 (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T},
                  Int64, Ptr{Cvoid}),
@@ -455,7 +457,7 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
     iters = ROCVector{Int32}(undef, N)
     err = ROCMatrix{T}(undef, N, 3)
     prm = KinIkParams(max_iters, lambda, tol_pos, tol_rot, max_step, rpy_objective ? 2 : 1, restarts, seed, 0,
-                      index_base)
+                      index_base, 0.0)
     if use_bistage
         check(ccall((:kin_ik_dls_batch_from, libkinhip), Cint,
                     (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T},

@@ -73,7 +73,8 @@ class CollDesc(C.Structure):
 class IkParams(C.Structure):
     _fields_ = [("max_iters", C.c_int32), ("lam", C.c_double), ("tol_pos", C.c_double),
                 ("tol_rot", C.c_double), ("max_step", C.c_double), ("with_rot", C.c_int32),
-                ("restarts", C.c_int32), ("seed", C.c_uint64), ("lanes", C.c_int32), ("index_base", C.c_int64)]
+                ("restarts", C.c_int32), ("seed", C.c_uint64), ("lanes", C.c_int32), ("index_base", C.c_int64),
+                ("damp_err", C.c_double)]
 
 
 class IkCollParams(C.Structure):

@@ -334,7 +334,8 @@ class Plan:
         return poses, jac
 
     def ik_dls(self, targets: torch.Tensor, Q: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None, Q0=None):
+               max_step=0.5, with_rot=True, restarts=0, seed=0, lanes=0, index_base=0, stream=None, Q0=None,
+               damp_err=0.0):
         """Batched DLS IK in place on Q; returns (Q, iters int32 [N], err [2, N]).  `lanes`: lanes per
         target running restart attempts side by side (0 auto, which runs batches of more than one round
         of waves in two phases: attempt 0 of every target, then the other attempts of the unsolved ones;
@@ -346,7 +347,9 @@ class Plan:
         call, without the copy.
         `with_rot`: 0 position only, 1 (True) axis-angle residual, 2 the reference's objective
         (src/inverse_kinematics.jl:38-50: [p* - p; rpy* - rpy] with the rpy_jac Jacobian; `tol_rot`
-        then bounds |d rpy| and err[1] is |d rpy|)."""
+        then bounds |d rpy| and err[1] is |d rpy|).
+        `damp_err`: error-scaled damping -- each iteration solves with lam^2 + damp_err (|dp|^2 + |rot|^2)
+        (Levenberg-Marquardt after Sugihara; 0: fixed lam)."""
         N = self._check_q(Q)
         if Q0 is not None:
             _same_device(Q0, Q, "Q0")
@@ -358,7 +361,7 @@ class Plan:
         iters = torch.empty(N, dtype=torch.int32, device=Q.device)
         err = torch.empty((2, N), dtype=self.dtype, device=Q.device)
         prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
-                         int(restarts), int(seed), int(lanes), int(index_base))
+                         int(restarts), int(seed), int(lanes), int(index_base), float(damp_err))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         if Q0 is not None:
             K.check(K.lib().kin_ik_dls_batch_from(self._h, C.byref(prm), targets.data_ptr(), N, Q0.data_ptr(),

@@ -726,6 +726,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                  * unconstrained direction J_k^T y decides the set of the next iteration */
                 {
                     double A[36], y[6];
+                    const double lam2 = prm->lambda * prm->lambda + prm->damp_err * (ep * ep + er * er);
                     for (int r = 0; r < rows; ++r) y[r] = e[r];
                     for (int32_t k = 0; k < ndof; ++k)
                         for (int r = 0; r < rows; ++r) Jw[r + rows * k] = held[k] ? 0.0 : J[r + rows * k];
@@ -733,7 +734,7 @@ void or_ik_dls_batch(const or_mech* proto, int64_t n, double* q, int64_t ldq, in
                         for (int r = 0; r < rows; ++r) {
                             double s = 0;
                             for (int32_t k = 0; k < ndof; ++k) s += Jw[r + rows * k] * Jw[c + rows * k];
-                            A[r + rows * c] = s + (r == c ? prm->lambda * prm->lambda : 0.0);
+                            A[r + rows * c] = s + (r == c ? lam2 : 0.0);
                         }
                     chol_solve(A, rows, y);
                     for (int32_t k = 0; k < ndof; ++k) {

@@ -114,6 +114,7 @@ typedef struct {
                           residual (wrapped) with the rpy_jac Jacobian (src/inverse_kinematics.jl:38-50) */
     int32_t restarts;  /* attempts = restarts + 1, each max_iters / attempts iterations */
     uint64_t seed;     /* re-seed stream: ik_seed_u01(seed, config index, attempt, column) */
+    double damp_err;   /* error-scaled damping: lambda^2 + damp_err * (|dp|^2 + |rot|^2) (0: fixed lambda) */
 } or_ik_params;
 /* the restart re-seed draw in [0, 1) shared by the oracle and the GPU kernel */
 double or_ik_seed_u01(uint64_t seed, int64_t i, int32_t attempt, int32_t col);

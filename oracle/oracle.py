@@ -148,7 +148,7 @@ class _Desc(C.Structure):
 class _IkParams(C.Structure):
     _fields_ = [("max_iters", C.c_int32), ("lam", C.c_double), ("tol_pos", C.c_double),
                 ("tol_rot", C.c_double), ("max_step", C.c_double), ("with_rot", C.c_int32),
-                ("restarts", C.c_int32), ("seed", C.c_uint64)]
+                ("restarts", C.c_int32), ("seed", C.c_uint64), ("damp_err", C.c_double)]
 
 
 _lib = None
@@ -329,14 +329,15 @@ class OracleMech:
         return q
 
     def ik_dls_batch(self, q0, q_joint_ids, link_id, target, max_iters=64, lam=1e-2, tol_pos=1e-3,
-                     tol_rot=1e-3, max_step=0.5, with_rot=True, restarts=0, seed=0, n_threads=0):
+                     tol_rot=1e-3, max_step=0.5, with_rot=True, restarts=0, seed=0, n_threads=0, damp_err=0.0):
         q = _f64(q0).copy()
         ids = _i32(q_joint_ids)
         tgt = _f64(target)
         N = q.shape[1]
         it = np.zeros(N, np.int32)
         err = np.zeros((2, N))
-        prm = _IkParams(max_iters, lam, tol_pos, tol_rot, max_step, int(with_rot), int(restarts), int(seed))
+        prm = _IkParams(max_iters, lam, tol_pos, tol_rot, max_step, int(with_rot), int(restarts), int(seed),
+                        float(damp_err))
         lib().or_ik_dls_batch(self._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt), tgt.shape[1],
                               C.byref(prm), _p(it), _p(err), n_threads)
         return q, it, err

@@ -453,8 +453,9 @@ def test_ik_dls_lanes_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0].cpu().numpy(), rq, atol=1e-7)
 
 
-@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
+@pytest.mark.parametrize("dtype,damp_err", [(torch.float64, 0.0), (torch.float32, 0.0), (torch.float64, 0.01),
+                                            (torch.float32, 0.01)])
+def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype, damp_err):
     """The two-phase schedule (automatic for this batch: 65,536 targets, 6 attempts of 4 iterations)
     returns the single-phase schedules' angles, iteration counts and errors bit for bit (lanes=1:
     sequential attempts, lanes=4: side by side), and fp64 matches the oracle on a subset."""
@@ -468,7 +469,7 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
     if dtype == torch.float32:
         plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
     T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
-    kw = dict(max_iters=23, restarts=4, seed=5, lam=1e-2, max_step=0.5)
+    kw = dict(max_iters=23, restarts=4, seed=5, lam=1e-2, max_step=0.5, damp_err=damp_err)
     res = [plan.ik_dls(T, torch.zeros((8, N), dtype=dtype, device=dev), lanes=lanes, **kw) for lanes in (0, 1, 4)]
     it0 = res[0][1].cpu().numpy()
     assert len(set((it0 // 4).tolist())) > 3  # winners spread over several attempts: phase 2 does work
@@ -481,12 +482,14 @@ def test_ik_dls_two_phase_identical(dev, fetch_tree, dtype):
         np.testing.assert_allclose(res[0][0][:, :k].cpu().numpy(), rq, atol=1e-7)
 
 
-def test_ik_dls_spec_two_phase_fp64_vs_oracle(dev, fetch_tree):
+@pytest.mark.parametrize("damp_err,max_step", [(0.0, 0.5), (0.01, 1.0)])
+def test_ik_dls_spec_two_phase_fp64_vs_oracle(dev, fetch_tree, damp_err, max_step):
     """Config 4's schedule in fp64 on the specialised kernels (two-phase with the hand-over; phase 2's
     lane-group minimum, ring prefix and ring lookup by DPP / v_readlane): bit-identical to the one-phase
     schedules of the same compilation (lanes 1 and 4) and to itself over repeated calls (the rings'
     control words carry over), and the first 1,000 targets equal the oracle restatement (equal
-    iteration counts, angles to 1e-7)."""
+    iteration counts, angles to 1e-7) -- with a fixed lambda and with the error-scaled damping
+    (kin_ik_params.damp_err, config 4's bench setting)."""
     m, arm = _fetch()
     gl = m.find_link("gripper_link")
     ids = [j.id for j in arm]
@@ -496,7 +499,7 @@ def test_ik_dls_spec_two_phase_fp64_vs_oracle(dev, fetch_tree):
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float64)
     plan.specialize(kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
     T = torch.tensor(tgt, dtype=torch.float64, device=dev).contiguous()
-    kw = dict(max_iters=64, restarts=3, seed=7, lam=1e-2, max_step=0.5)
+    kw = dict(max_iters=64, restarts=3, seed=7, lam=1e-2, max_step=max_step, damp_err=damp_err)
     Z = torch.zeros((8, N), dtype=torch.float64, device=dev)
     ref = plan.ik_dls(T, Z.clone(), lanes=0, **kw)
     assert (ref[1] > 16).any()  # phase 2 did work
