@@ -250,7 +250,9 @@ typedef struct kin_ik_params {
                            Jacobian; 2: the reference's f_objective (src/inverse_kinematics.jl:38-50): residual
                            [p* - p; rpy(target) - rpy(pose)] (angle differences wrapped to (-pi, pi]) with the
                            rpy_jac=true Jacobian, converged when |dp| < tol_pos and |d rpy| < tol_rot (err row 1
-                           is then |d rpy|) */
+                           is then |d rpy|).  The wrap deviates from the reference on purpose: its raw difference
+                           is ~2 pi when the two yaws (or rolls) lie on either side of +-pi, which sends the arm
+                           the long way round; tests/test_gpu_ik_rpy.py::test_rpy_difference_wraps_at_pi */
     int32_t restarts;   /* 0: none; else max_iters is split into restarts+1 attempts and each new
                            attempt re-draws the relevant joints uniformly within their limits
                            (U[-pi, pi] if unbounded) from a counter hash of (seed, i, attempt, column) */

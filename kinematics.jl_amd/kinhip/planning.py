@@ -271,8 +271,11 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
     ftol_abs rule (``_dls_ik_ftol``), stage 2 the batched collision-aware kernel
     (``CollisionIKPlan.ik_coll``, kin_ik_coll_batch: the reference's rpy objective plus the
     IneqConst(sscc, joints, sdf, 1, margin) sphere rows, 3 seeded restarts) on a batch of one, converged
-    to |dp|, |d rpy| < 1e-6 with every sphere at >= margin - 1e-6 (status ``:FTOL_REACHED``, else
-    ``:MAXEVAL_REACHED``).
+    to |dp|, |d rpy| < 1e-6 with every sphere at >= margin - 1e-6 (status ``:FTOL_REACHED``).  When no
+    attempt converges (a pose the constraint forbids) the kernel returns the attempt whose end state has
+    the lowest merit |dp|^2 + |d rpy|^2 + max(0, margin - min d)^2 (the penalty problem's value; ties: the
+    earlier attempt, so the stage-1-seeded attempt 0 wins over equal restarts), status
+    ``:MAXEVAL_REACHED``.  ``ftol`` applies to stage 1 only: stage 2 is judged on the 1e-6 rule above.
     ``solver="SLSQP"``: stage 2 by SciPy's SLSQP on the host (the reference uses NLopt's LD_SLSQP), one
     GPU evaluation per iterate, ``ftol`` as the reference's ftol_abs."""
     from .collision import CollisionIKPlan

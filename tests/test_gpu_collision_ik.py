@@ -301,3 +301,53 @@ def test_collision_ik_lanes_identical(spec, dtype):
         # the case exercises the schedule: targets solved in attempt 0, in a restart, and not at all
         L = max_iters // (restarts + 1)
         assert (it <= L).any() and ((it > L) & (it <= max_iters)).any(), np.bincount(np.minimum(it, max_iters + 1))
+
+
+def _merit(m, gl, arm, sscc, sdf, T, margin=0.02):
+    Tn = kinhip.get_transform(m, gl)
+    d = kinhip.compute_coll_dists(sscc, arm, sdf)
+    dp = np.linalg.norm(Tn[:3, 3] - T[:3, 3])
+    dr = _ypr(Tn) - _ypr(T)
+    dr = (dr + np.pi) % (2 * np.pi) - np.pi
+    return dp ** 2 + float(dr @ dr) + max(0.0, margin - d.min()) ** 2, dp, d.min()
+
+
+def test_infeasible_target_returns_the_best_attempt_vs_slsqp():
+    """a pose the constraint forbids (an 8 cm box around the gripper's target point): the DLS
+    stage 2 reports :MAXEVAL_REACHED with its best attempt -- not the last restart's end state -- and that
+    answer's merit (pose error^2 + margin violation^2, what the kernel ranks attempts by) is no worse than
+    what SciPy's SLSQP (the reference's solver family, constraint enforced) reaches from the same stage-1
+    seed, up to a small slack; the SLSQP path itself ends feasible."""
+    m, arm, sscc, sdf0 = _scene()
+    gl = m.find_link("gripper_link")
+    T = _pose((0.75, 0.15, 1.0))
+    sdf = kinhip.UnionSDF(sdf0.sdfs + [kinhip.BoxSDF(_pose((0.75, 0.15, 1.0)), (0.08, 0.08, 0.08))])
+    m.set_joint_angles(arm, np.zeros(8))
+    q, status = kinhip.inverse_kinematics_(m, gl, arm, T, sscc, sdf, use_bistage=True)
+    f_dls, dp_dls, dmin_dls = _merit(m, gl, arm, sscc, sdf, T)
+    m.set_joint_angles(arm, np.zeros(8))
+    q2, st2 = kinhip.inverse_kinematics_(m, gl, arm, T, sscc, sdf, use_bistage=True, solver="SLSQP")
+    f_sq, dp_sq, dmin_sq = _merit(m, gl, arm, sscc, sdf, T)
+    print(f"DLS {status}: merit {f_dls:.3e} |dp| {dp_dls:.3e} min d {dmin_dls:.4f}; "
+          f"SLSQP {st2}: merit {f_sq:.3e} |dp| {dp_sq:.3e} min d {dmin_sq:.4f}")
+    assert status == ":MAXEVAL_REACHED"
+    assert np.all(np.isfinite(q))
+    assert f_dls <= 1.5 * f_sq + 1e-4, (f_dls, f_sq)
+    assert dmin_sq >= 0.02 - 1e-4  # SLSQP keeps the constraint (to its feasibility tolerance)
+
+
+def test_slsqp_stage2_pose_accuracy_at_ftol():
+    """the SLSQP stage 2 takes ftol as SciPy's ftol (the reference's ftol_abs = 1e-5 on
+    f = |residual|^2): on a feasible target the pose still ends within the reference test's 1e-3."""
+    m, arm, sscc, sdf = _scene()
+    gl = m.find_link("gripper_link")
+    T = _pose((1.0, 0.0, 1.25))
+    m.set_joint_angles(arm, np.zeros(8))
+    q, status = kinhip.inverse_kinematics_(m, gl, arm, T, sscc, sdf, use_bistage=True, solver="SLSQP")
+    Tn = kinhip.get_transform(m, gl)
+    d = kinhip.compute_coll_dists(sscc, arm, sdf)
+    print(f"SLSQP {status}: |dp| {np.linalg.norm(Tn[:3, 3] - T[:3, 3]):.2e} min d {d.min():.4f}")
+    assert status == ":FTOL_REACHED"
+    assert np.linalg.norm(Tn[:3, 3] - T[:3, 3]) < 1e-3
+    assert np.linalg.norm(_ypr(Tn) - _ypr(T)) < 1e-3
+    assert d.min() >= 0.02 - 1e-4

@@ -117,3 +117,46 @@ def test_with_rot_out_of_range_is_refused(dev):
     with pytest.raises(kinhip.KinError):
         plan.ik_dls(torch.zeros((12, 4), dtype=torch.float32, device=dev), torch.zeros((8, 4), dtype=torch.float32,
                                                                                      device=dev), with_rot=3)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_rpy_difference_wraps_at_pi(dev, dtype):
+    """the kernel (and the oracle) wrap each rpy difference to (-pi, pi] -- a deliberate
+    deviation from src/inverse_kinematics.jl:42, whose raw rpy(target) - rpy(pose) is ~2 pi when the two
+    yaws sit on either side of +-pi (the objective then pulls the arm the long way round).  Pinned here:
+    targets whose yaw is the start pose's yaw turned 0.04 rad across +-pi have |d rpy| = 0.04 at the start
+    (not 2 pi - 0.04), and the solve converges within a few iterations, equal to the oracle in fp64."""
+    m = kinhip.parse_urdf(golden("fetch.urdf"))
+    arm = [m.find_joint(n) for n in ARM]
+    gl = m.find_link("gripper_link")
+    om = O.OracleMech(O.parse_urdf_tree(golden("fetch.urdf")))
+    ids = [j.id for j in arm]
+    lo = np.nan_to_num(np.array([j.lower_limit for j in arm]), neginf=-np.pi)
+    hi = np.nan_to_num(np.array([j.upper_limit for j in arm]), posinf=np.pi)
+    rng = np.random.default_rng(3)
+    q = lo[:, None] + (hi - lo)[:, None] * rng.random((8, 20000))
+    P = om.fk_batch(q, ids, [gl.id])[0]
+    yaw = np.arctan2(P[1], P[0])  # RotZYX yaw of the column-major rotation (R21, R11)
+    pick = np.where((np.abs(yaw) > np.pi - 0.015) & (np.sqrt(np.maximum(0, 1 - P[2] ** 2)) > 0.5))[0][:64]
+    assert pick.size >= 16
+    q0 = q[:, pick]
+    N = pick.size
+    tgt = np.empty((12, N))
+    for k in range(N):
+        d = 0.04 if yaw[pick[k]] > 0 else -0.04  # across +-pi
+        Rz = np.array([[np.cos(d), -np.sin(d), 0], [np.sin(d), np.cos(d), 0], [0, 0, 1.0]])
+        R = P[:9, pick[k]].reshape(3, 3).T  # column-major -> R
+        tgt[:9, k] = (Rz @ R).T.reshape(-1)
+        tgt[9:, k] = P[9:, pick[k]]
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
+    Q0 = torch.tensor(q0, dtype=dtype, device=dev).contiguous()
+    _, _, e0 = plan.ik_dls(T, Q0.clone(), max_iters=0, with_rot=2, tol_pos=0.0, tol_rot=0.0)
+    np.testing.assert_allclose(e0[1].double().cpu().numpy(), 0.04, atol=1e-5)  # wrapped, not 2 pi - 0.04
+    kw = dict(max_iters=16, lam=1e-2, max_step=0.5, tol_pos=1e-6, tol_rot=1e-6, with_rot=2)
+    Q, it, _ = plan.ik_dls(T, Q0.clone(), **kw)
+    assert (it.cpu().numpy() <= 8).all(), it
+    if dtype == torch.float64:
+        rq, rit, rerr = om.ik_dls_batch(q0, ids, gl.id, tgt, **kw)
+        np.testing.assert_array_equal(it.cpu().numpy(), rit)
+        np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
