@@ -14,7 +14,7 @@ import kinhip  # noqa: E402
 
 ap = argparse.ArgumentParser()
 BASE = ["fkjac32", "fkjac32t", "fkjac64", "fkjac64t", "fk6_64", "fk6_64t", "ik32", "ik64", "coll32", "collg32", "collg32t",
-        "coll64", "scene32", "cik32"]
+        "coll64", "scene32", "cik32", "cikp32"]
 ap.add_argument("--what", default="fkjac32", choices=BASE + [w + "s" for w in BASE],
                 help="workload; a trailing 's' runs the plan-specialised kernels (kin_plan_specialize)")
 ap.add_argument("--steps", type=int, default=20)

@@ -25,6 +25,9 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
     "fkjac64t": ("k_fk<double, 8>", (8 + 12 + 48) * 8 * (1 << 20), "FK + 6x8 J, fp64, N = 2^20, tiled SoA (tile 4096)"),
     "fkjac32s": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
                  "FK + 6x8 J, fp32, N = 2^20, plain SoA rows padded by 256, plan-specialised kernel"),
+    "fkjac32sjl": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
+                   "FK + 6x8 J, fp32, N = 2^20, plain SoA rows with ld = N (the Julia shim's ROCMatrix(N, 8) / "
+                   "ROCArray(N, 6, 8)), plan-specialised kernel (bench fk_jac_f32_julia_layout)"),
     "fkjac32ts": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 20),
                   "FK + 6x8 J, fp32, N = 2^20, tiled SoA (tile 8192), plan-specialised kernel (bench headline)"),
     "fkjac32ts22": ("kinhip_jit_fk_f32", (8 + 12 + 48) * 4 * (1 << 22),
