@@ -594,18 +594,25 @@ def _pattern_us(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0, per
     return us
 
 
-def _cold_leg(leg, n, stream, bytes_per_eval, reps=10):
+def _cold_leg(leg, n, stream, bytes_per_eval, reps=10, tiled=True):
     """One launch at a time after a 1 GiB read (torch sum) has evicted the Infinity Cache: the
-    launch's own HIP events bracket it alone (the read is outside them)."""
+    launch's own HIP events bracket it alone (the read is outside them).  `leg`: (plan, q, poses, jac)
+    in the tiled layout (kin_plan_run_tiled) or, with tiled=False, plain SoA rows (kin_plan_run)."""
     plan, Qt, P, J = leg
+
+    def run():
+        if tiled:
+            plan.run_tiled(Qt, n, P, J, stream=stream)
+        else:
+            plan.run(Qt, P, J, stream=stream)
     scrub = torch.ones(1 << 28, dtype=torch.float32, device=Qt.device)
     e = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     with torch.cuda.stream(stream):
-        plan.run_tiled(Qt, n, P, J, stream=stream)
+        run()
         for e0, e1 in e:
             scrub.sum()
             e0.record(stream)
-            plan.run_tiled(Qt, n, P, J, stream=stream)
+            run()
             e1.record(stream)
     torch.cuda.synchronize()
     t = sum(a.elapsed_time(b) for a, b in e) / reps / 1e3
@@ -766,6 +773,17 @@ def main():
         out["fk_jac_f32_generic_plain_soa"] = {"value": N * ws * args.steps / wg, "unit": "evals/s",
                                                "avg_launch_us": dg / args.steps * 1e6,
                                                "achieved_GBs": bytes_per_eval * N / (dg / args.steps) / 1e9}
+    if args.extras:
+        # the layout the Julia shim's get_jacobian! hands over (KinematicsHIP.jl: ROCMatrix(N, 8) /
+        # ROCArray(N, 6, 8) -> plain SoA rows with ld = N, unpadded), warm like the headline and cold
+        wj, dj = timed_leg(torch.float32, True, [gl], "soa_pad0")
+        aj = bytes_per_eval * N / (dj / args.steps) / 1e9
+        out["fk_jac_f32_julia_layout"] = {
+            "value": N * ws * args.steps / wj, "unit": "evals/s", "avg_launch_us": dj / args.steps * 1e6,
+            "achieved_GBs": aj, "frac": aj / HBM_PEAK_GBS, "vs_headline": (N * ws * args.steps / wj) / value,
+            "layout": "plain SoA, ld = N (unpadded)",
+            "kernels": "specialised" if headline_spec else "generic",
+            "cold_cache": _cold_leg(leg(torch.float32, True, [gl], pad=0), N, stream, bytes_per_eval, tiled=False)}
     if args.sweep:
         # the same workload in the other layouts: plain SoA (padded and unpadded rows), other tiles
         lay = {}
