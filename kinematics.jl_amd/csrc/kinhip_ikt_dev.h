@@ -73,12 +73,13 @@ __device__ __forceinline__ void sphere_row(const KIkcProg<T>& P, uint32_t anc, T
     const T w0 = fma(py, g[2], -(pz * g[1]));
     const T w1 = fma(pz, g[0], -(px * g[2]));
     const T w3 = fma(px, g[1], -(py * g[0]));
+    const bool base = P.base_col >= 0;  // (base_col = -1 without a base: no variable is a base column)
 #pragma unroll
     for (int v = 0; v < MAXV; ++v) {
         T x;
-        if (v == P.base_col) x = g[0];
-        else if (v == P.base_col + 1) x = g[1];
-        else if (P.base_col >= 0 && v == P.base_col + 2) x = fma(-g[0], py - b[1], g[1] * (px - b[0]));
+        if (base && v == P.base_col) x = g[0];
+        else if (base && v == P.base_col + 1) x = g[1];
+        else if (base && v == P.base_col + 2) x = fma(-g[0], py - b[1], g[1] * (px - b[0]));
         else if ((P.prism_mask >> v) & 1u) x = fma(g[0], rz[v][0], fma(g[1], rz[v][1], g[2] * rz[v][2]));
         else
             x = fma(rz[v][0], w0, fma(rz[v][1], w1, fma(rz[v][2], w3,
