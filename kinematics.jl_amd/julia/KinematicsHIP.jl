@@ -203,22 +203,37 @@ end
 
 stream_ptr() = AMDGPU.stream().stream
 
+# Device batches: a ROCArray, or a view of one whose first dimension is contiguous (a padded batch from
+# batch_array); pointer() and stride(A, 2) give the C-ABI's base pointer and leading dimension.
+const DevMat{T} = Union{ROCMatrix{T},SubArray{T,2,<:ROCArray{T}}}
+const DevArr3{T} = Union{ROCArray{T,3},SubArray{T,3,<:ROCArray{T}}}
+
+"""`batch_array(T, N, dims...)`: an (N, dims...) device batch in the C-ABI's SoA layout (configuration index
+fastest) whose leading dimension is padded to N + 256.  Use it for Q, J and poses at batch sizes that are
+powers of two: rows exactly 2^k elements apart fall on the same Infinity-Cache sets and lose the cache's
+reuse between launches (2^20 FK + J: 47.5 us with ld = N against 41 us padded, DESIGN.md section 3).  A
+view of the first N rows; passed zero-copy."""
+function batch_array(::Type{T}, N::Integer, dims::Integer...; pad::Integer=256) where {T}
+    A = ROCArray{T}(undef, N + pad, dims...)
+    view(A, 1:N, ntuple(_ -> Colon(), length(dims))...)
+end
+
 """Batched `get_transform`: poses[:, :, k] = world pose (3x4, column-major) of links[k] for every row of Q."""
 function Kinematics.get_transform(hm::HIPModel, links::Vector{<:Link}, joints::Vector{<:Joint},
-                                  Q::ROCMatrix{T}) where {T<:Union{Float32,Float64}}
+                                  Q::DevMat{T}) where {T<:Union{Float32,Float64}}
     N = size(Q, 1)
-    poses = ROCArray{T}(undef, N, 12, length(links))
+    poses = batch_array(T, N, 12, length(links))  # (padded rows, see batch_array)
     p = plan!(hm, T, Int32[j.id for j in joints], Int32[l.id for l in links], Int32(0), Int32[], UInt32(0))
     check(ccall((:kin_plan_run, libkinhip), Cint,
                 (Ptr{Cvoid}, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
-                p, pointer(Q), stride(Q, 2), N, pointer(poses), N, C_NULL, 0, stream_ptr()))
+                p, pointer(Q), stride(Q, 2), N, pointer(poses), stride(poses, 2), C_NULL, 0, stream_ptr()))
     poses
 end
 
 """Batched `get_jacobian!`: J[i, :, :] is mat_out of configuration i; untouched entries keep their values."""
 function Kinematics.get_jacobian!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool,
-                                  J::ROCArray{T,3}, Q::ROCMatrix{T}; rpy_jac=false,
-                                  pose::Union{Nothing,ROCArray{T,3}}=nothing) where {T<:Union{Float32,Float64}}
+                                  J::DevArr3{T}, Q::DevMat{T}; rpy_jac=false,
+                                  pose::Union{Nothing,DevArr3{T}}=nothing) where {T<:Union{Float32,Float64}}
     N = size(Q, 1)
     flags = (with_rot ? KIN_WITH_ROT : UInt32(0)) | (rpy_jac ? KIN_RPY_JAC : UInt32(0))
     ids = Int32[j.id for j in joints]
@@ -226,8 +241,8 @@ function Kinematics.get_jacobian!(hm::HIPModel, link::Link, joints::Vector{<:Joi
     p = plan!(hm, T, ids, outs, Int32(link.id), ids, flags)
     check(ccall((:kin_plan_run, libkinhip), Cint,
                 (Ptr{Cvoid}, Ptr{T}, Int64, Int64, Ptr{T}, Int64, Ptr{T}, Int64, Ptr{Cvoid}),
-                p, pointer(Q), stride(Q, 2), N, pose === nothing ? C_NULL : pointer(pose), N, pointer(J), N,
-                stream_ptr()))
+                p, pointer(Q), stride(Q, 2), N, pose === nothing ? C_NULL : pointer(pose),
+                pose === nothing ? N : stride(pose, 2), pointer(J), stride(J, 2), stream_ptr()))
     J
 end
 
@@ -505,6 +520,6 @@ function pose_const!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot
     vals, jac
 end
 
-export HIPModel, sync!, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
+export HIPModel, sync!, batch_array, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
 
 end # module
