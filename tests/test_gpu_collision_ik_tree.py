@@ -92,7 +92,14 @@ class Scene:
         return [self.om.get_transform(s)[:3, 3] for s in self.sph]
 
     def check(self, link, tg, Q1, sdf, box=None, boxes=None, spec=False, lanes=0, scene_q=None, kw=KW,
-              min_conv=0.5):
+              min_conv=0.5, knife_edge=0.01):
+        """GPU vs oracle.  Equal iteration counts on all but `knife_edge` of the targets: a sphere the penalty
+        holds at the band's edge (d -> margin + band, where its row switches on and off) sits on a
+        switching surface, and last-bit differences between the kernel's FMA sums and the oracle's can
+        flip its row on a step -- the two runs then part.  On the targets with equal counts: converged
+        answers' angles within 1e-7 and err rows within 1e-9; unconverged ones return the lowest-merit
+        attempt, and attempts that end in the same constrained minimum tie in merit to the last bits, so
+        there the merits (from the err rows) agree to 1e-9 while the angles may be another tying attempt's."""
         plan = kinhip.CollisionIKPlan(self.sscc, self.m.find_link(link), self.q, dtype=torch.float64)
         if spec:
             plan.specialize()
@@ -102,11 +109,20 @@ class Scene:
         rq, rit, rerr = self.O.ik_coll_batch(self.om, box, Q1.cpu().numpy(), self.ids, self.tree.link_id(link), tg,
                                              self.sph, self.rad, sdfs=boxes, sphere_parents=self.par, **kw)
         it = it.cpu().numpy()
+        q, e = Q.cpu().numpy(), err.cpu().numpy()
         conv = it <= kw["max_iters"]
         assert conv.mean() >= min_conv, conv.mean()
-        np.testing.assert_array_equal(it, rit)
-        np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
-        np.testing.assert_allclose(err.cpu().numpy(), rerr, atol=1e-9)
+        same = it == rit
+        assert (~same).mean() <= knife_edge, (np.where(~same)[0], it[~same], rit[~same])
+        c = same & conv
+        np.testing.assert_allclose(q[:, c], rq[:, c], atol=1e-7)
+        np.testing.assert_allclose(e[:, c], rerr[:, c], atol=1e-9)
+        u = same & ~conv
+        w2 = kw["weight"] ** 2
+
+        def merit(x):
+            return x[0] ** 2 + x[1] ** 2 + w2 * np.maximum(kw["margin"] - x[2], 0.0) ** 2
+        np.testing.assert_allclose(merit(e[:, u]), merit(rerr[:, u]), rtol=1e-9, atol=1e-12)
         return Q, it, err
 
 
@@ -175,10 +191,15 @@ def test_two_arm_tree(tmp_path, spec, lanes, with_base):
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(43)
     N = 300
-    tg = np.zeros((12, N))
-    for k in range(N):
-        tg[:, k] = _col(_pose((rng.uniform(0.35, 0.55), rng.uniform(0.15, 0.35), rng.uniform(0.95, 1.2)),
-                              rng.uniform(-0.4, 0.4)))
+    # reachable left-gripper poses (FK of random torso / left-arm angles, and base offsets): four arm joints
+    # and the torso cannot reach an arbitrary 6-D pose without the base
+    qt = np.zeros((sc.nd, N))
+    qt[4] = rng.uniform(0.05, 0.25, N)
+    qt[5:9] = np.stack([rng.uniform(-0.8, 0.8, N), rng.uniform(-0.6, 0.6, N), rng.uniform(-1.0, 1.0, N),
+                        rng.uniform(-1.2, 1.2, N)])
+    if with_base:
+        qt[9:12] = np.stack([rng.uniform(-0.2, 0.2, N), rng.uniform(-0.2, 0.2, N), rng.uniform(-0.3, 0.3, N)])
+    tg = sc.om.fk_batch(qt, sc.ids, [sc.tree.link_id("l_grip")])[0]
     Q1 = _stage1(sc, "l_grip", tg, dev)
     Q1[:4] = torch.tensor([0.3, 0.4, 0.0, 0.6], dtype=torch.float64, device=dev)[:, None]  # right arm start
     c = sc.sphere_centres(Q1[:, 0].cpu().numpy(), None)[6]  # r4's first sphere
