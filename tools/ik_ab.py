@@ -23,7 +23,8 @@ for dt in ((torch.float32,) if os.environ.get("AB_F32") else (torch.float32, tor
                                 dtype=dt, device=dev)
     tgt = plan.run(Qt)[0][0].contiguous()
     Q0 = torch.zeros((8, n), dtype=dt, device=dev)
-    kw = dict(max_iters=64, restarts=3, seed=0, lam=1e-2, max_step=0.5, tol_pos=1e-3, tol_rot=1e-3)
+    kw = dict(max_iters=64, restarts=3, seed=0, lam=1e-2, max_step=float(os.environ.get("IK_MAXSTEP", 0.5)),
+              damp_err=float(os.environ.get("IK_DAMP", 0.0)), tol_pos=1e-3, tol_rot=1e-3)
     Qs = [Q0.clone() for _ in range(12)]
     plan.ik_dls(tgt, Qs[0], **kw)
     torch.cuda.synchronize()
@@ -38,4 +39,5 @@ for dt in ((torch.float32,) if os.environ.get("AB_F32") else (torch.float32, tor
                f"mean_it {it.float().mean():.2f} qsum {float(Q.double().sum()):.6f}")
 print(os.path.basename(os.environ.get("KINHIP_LIB", "default")), "G=" + os.environ.get("KINHIP_IK_GROUP", "auto"),
       "Q=" + os.environ.get("KINHIP_IK_QUEUE", "auto"), "spec=" + os.environ.get("AB_SPEC", "0"),
+      f"max_step={kw['max_step']} damp_err={kw['damp_err']}",
       " | ".join(out), flush=True)
