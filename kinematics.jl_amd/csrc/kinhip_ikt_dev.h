@@ -133,6 +133,25 @@ __device__ __forceinline__ double row_group_min(double v) {
 __device__ __forceinline__ float lane_bcast(float v, int src) { return __int_as_float(__shfl(__float_as_int(v), src)); }
 __device__ __forceinline__ double lane_bcast(double v, int src) { return __shfl(v, src); }
 
+// value of lane l of each 16-lane DPP row for every lane of that row (v_mov_b32_dpp row_newbcast:l, a VALU
+// move instead of an LDS round trip); l must fold to a constant (the specialised kernels' unrolled loops)
+template <int CTL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTL, 0xF, 0xF, false));
+}
+template <typename T>
+__device__ __forceinline__ T row_bcast16(T v, int l) {
+#define KIN_RB(n) \
+    case n:       \
+        if constexpr (sizeof(T) == 4) return dpp_f32<0x150 + n>(v); else return dpp_f64<0x150 + n>(v);
+    switch (l) {
+        KIN_RB(0) KIN_RB(1) KIN_RB(2) KIN_RB(3) KIN_RB(4) KIN_RB(5) KIN_RB(6) KIN_RB(7)
+        KIN_RB(8) KIN_RB(9) KIN_RB(10) KIN_RB(11) KIN_RB(12) KIN_RB(13) KIN_RB(14)
+        default: if constexpr (sizeof(T) == 4) return dpp_f32<0x15F>(v); else return dpp_f64<0x15F>(v);
+    }
+#undef KIN_RB
+}
+
 // min over the G attempt groups of a target (lanes S apart): DPP inside a quad for S = 1, else
 // ds_bpermute (once per iteration)
 template <int G, int S>
@@ -391,12 +410,14 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                     if (rr == r) bal = inband[rr];
                 if ((bal >> src) & 1ull) {  // (uniform inside the attempt group)
                     T vk = T(0), ak[MAXV];
+                    // S = 16: the attempt group is one DPP row, and lane k % 16 of it broadcasts by DPP
+                    auto bc = [&](T x) { return S == 16 ? row_bcast16(x, k % 16) : lane_bcast(x, src); };
 #pragma unroll
                     for (int rr = 0; rr < NR; ++rr)
                         if (rr == r) {
-                            vk = lane_bcast(viol[rr], src);
+                            vk = bc(viol[rr]);
 #pragma unroll
-                            for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? lane_bcast(av[rr][v], src) : T(0);
+                            for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? bc(av[rr][v]) : T(0);
                         }
                     accum_row<T, MAXV>(A, bv, ak, vk, w2, anc);
                 }
@@ -508,15 +529,25 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         T y[MAXV];
 #pragma unroll
         for (int v = 0; v < MAXV; ++v) y[v] = ((freev >> v) & 1u) ? bv[v] : T(0);
-        // Cholesky (in place, lower) and the two triangular solves
+        // Cholesky (in place, lower) and the two triangular solves.  fp32: the reciprocal square root of
+        // each pivot (v_rsq_f32) multiplies instead of the IEEE square root and divisions (~10 instructions
+        // each, on the one-wave critical path); fp64 keeps the oracle's exact form (iterates to 1e-7)
+        constexpr bool fast = sizeof(T) == 4;
+        T ip[MAXV];
 #pragma unroll
         for (int j = 0; j < MAXV; ++j) {
             T d = A[j][j];
 #pragma unroll
             for (int k = 0; k < j; ++k) d = fma(-A[j][k], A[j][k], d);
-            d = sqrt_t(d);
-            A[j][j] = d;
-            const T id = T(1) / d;
+            T id;
+            if constexpr (fast) {
+                id = rsqrt_fast(d);
+                ip[j] = id;
+            } else {
+                d = sqrt_t(d);
+                A[j][j] = d;
+                id = T(1) / d;
+            }
 #pragma unroll
             for (int r = j + 1; r < MAXV; ++r) {
                 T sm = A[r][j];
@@ -530,14 +561,16 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             T sm = y[r];
 #pragma unroll
             for (int k = 0; k < r; ++k) sm = fma(-A[r][k], y[k], sm);
-            y[r] = sm / A[r][r];
+            if constexpr (fast) y[r] = sm * ip[r];
+            else y[r] = sm / A[r][r];
         }
 #pragma unroll
         for (int r = MAXV - 1; r >= 0; --r) {
             T sm = y[r];
 #pragma unroll
             for (int k = r + 1; k < MAXV; ++k) sm = fma(-A[k][r], y[k], sm);
-            y[r] = sm / A[r][r];
+            if constexpr (fast) y[r] = sm * ip[r];
+            else y[r] = sm / A[r][r];
         }
         T mx = T(0);
         uint32_t nh = 0;
