@@ -20,7 +20,10 @@ namespace {
 // in fp64 from the fp32 Jacobian.  Forming J J^T in fp32 errs by ~eps |J|^2 = 2.4e-7 against
 // lambda^2 = 1e-4, and at a singular arm (Fetch at q = 0: rank 4) y carries ~e / lambda^2 in the null
 // directions that J^T y cancels: an fp32 solve moves dq by up to 2e-3 rad against the fp64 oracle's,
-// the J rounding alone by 1e-6 (tools/ik_fp32_solve_error.py).  0: the fp32 solve (A/B build).
+// the J rounding alone by 1e-6 (tools/ik_fp32_solve_error.py).  0: the fp32 solve (A/B build).  2: the
+// fp32 factorisation and solve plus one step of iterative refinement whose residual
+// e - (J W J^T + lambda'^2 I) y is formed in fp64 from J itself (J^T y, then J (W J^T y)), never from
+// the rounded J J^T: the fp32 factor contracts the error by ~eps kappa ~ 1e-3 per step.
 #ifndef KINHIP_IK_F64SOLVE
 #define KINHIP_IK_F64SOLVE 1
 #endif
@@ -543,7 +546,9 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
 
         KIN_IK_STAMP(2);
         // the damped solve's arithmetic type: fp64 (also in the fp32 kernel, KINHIP_IK_F64SOLVE)
-        using TS = typename ik_solve_type<sizeof(T) == 4 && !KINHIP_IK_F64SOLVE>::type;
+        using TS = typename ik_solve_type<sizeof(T) == 4 && KINHIP_IK_F64SOLVE != 1>::type;
+        constexpr bool refine = sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 2;
+        using YS = typename ik_solve_type<!refine && sizeof(TS) == 4>::type;  // type of the solution y
         TS Jb[3][ROWS];
         if (base) {
 #pragma unroll
@@ -683,22 +688,66 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                     else A[r][j] = sm / d;
                 }
             }
-            TS y[ROWS];
+            auto chol_solve = [&](const TS (&rhs)[ROWS], TS (&x)[ROWS]) {
 #pragma unroll
-            for (int r = 0; r < ROWS; ++r) {
-                TS sm = (TS)e[r];
+                for (int r = 0; r < ROWS; ++r) {
+                    TS sm = rhs[r];
 #pragma unroll
-                for (int k = 0; k < r; ++k) sm = fma(-A[r][k], y[k], sm);
-                if constexpr (fast) y[r] = sm * ip[r];
-                else y[r] = sm / A[r][r];
-            }
+                    for (int k = 0; k < r; ++k) sm = fma(-A[r][k], x[k], sm);
+                    if constexpr (fast) x[r] = sm * ip[r];
+                    else x[r] = sm / A[r][r];
+                }
 #pragma unroll
-            for (int r = ROWS - 1; r >= 0; --r) {
-                TS sm = y[r];
+                for (int r = ROWS - 1; r >= 0; --r) {
+                    TS sm = x[r];
 #pragma unroll
-                for (int k = r + 1; k < ROWS; ++k) sm = fma(-A[k][r], y[k], sm);
-                if constexpr (fast) y[r] = sm * ip[r];
-                else y[r] = sm / A[r][r];
+                    for (int k = r + 1; k < ROWS; ++k) sm = fma(-A[k][r], x[k], sm);
+                    if constexpr (fast) x[r] = sm * ip[r];
+                    else x[r] = sm / A[r][r];
+                }
+            };
+            TS e_s[ROWS], y0[ROWS];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) e_s[r] = (TS)e[r];
+            chol_solve(e_s, y0);
+            YS y[ROWS];
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) y[r] = (YS)y0[r];
+            if constexpr (refine) {
+                // r = e - lambda'^2 y - J W (J^T y) - Jb Jb^T y in fp64, from the weighted columns of A
+                double res[ROWS];
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) res[r] = fma(-(double)lam2, y[r], (double)e[r]);
+#pragma unroll
+                for (int s = 0; s < MAXA; ++s) {
+                    T J[ROWS];
+                    jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
+                    if ((S[s].flags & SF_REC) && S[s].qcol >= 0 && ((blk >> s) & 1u)) continue;  // held: W = 0
+                    const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;
+                    double u = 0.0;
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r)
+                        if (r < nr) u = fma((double)J[r], y[r], u);
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r)
+                        if (r < nr) res[r] = fma(-(double)J[r], u, res[r]);
+                }
+                if (base) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        double u = 0.0;
+#pragma unroll
+                        for (int r = 0; r < ROWS; ++r) u = fma((double)Jb[k][r], y[r], u);
+#pragma unroll
+                        for (int r = 0; r < ROWS; ++r) res[r] = fma(-(double)Jb[k][r], u, res[r]);
+                    }
+                }
+                TS rs[ROWS], dl[ROWS];
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) rs[r] = (TS)res[r];
+                chol_solve(rs, dl);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) y[r] = y[r] + (YS)dl[r];
             }
             KIN_IK_STAMP(4);
             uint32_t nb = 0;
@@ -706,11 +755,11 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
                 jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
-                TS vs = TS(0);
+                YS vs = YS(0);
                 const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;  // (zero angular rows)
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
-                    if (r < nr) vs = fma((TS)J[r], y[r], vs);
+                    if (r < nr) vs = fma((YS)J[r], y[r], vs);
                 const T v = (T)vs;
                 const bool held = (blk >> s) & 1u;
                 dq[s] = held ? T(0) : v;
@@ -723,9 +772,9 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             if (base) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
-                    TS v = TS(0);
+                    YS v = YS(0);
 #pragma unroll
-                    for (int r = 0; r < ROWS; ++r) v = fma(Jb[k][r], y[r], v);
+                    for (int r = 0; r < ROWS; ++r) v = fma((YS)Jb[k][r], y[r], v);
                     db[k] = (T)v;
                     mx = fmax(mx, fabs(db[k]));
                 }

@@ -81,7 +81,8 @@ __global__ __launch_bounds__(256) void p_pattern_strided(const float* __restrict
 }
 
 template <int RI, int RO, bool SOFF>
-int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, hipStream_t st) {
+int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, int lds,
+                   hipStream_t st) {
     const bool tiled = tile > 0;
     if (tiled && tile % 256) return -1;
     // tiled arrays: (ntiles, rows, tile) -- a tile of q is RI rows, a tile of out RO rows
@@ -90,11 +91,13 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
     if ((uint64_t)(tiled ? tile : n) * 4u >= (1ull << 31)) return -1;  // 32-bit lane offsets
     if (SOFF && (uint64_t)(RO * ldr + (tiled ? tile : n)) * 4u >= (1ull << 31)) return -1;
     const unsigned units = (unsigned)((n + 255) / 256);
+    // lds: dynamic LDS bytes per workgroup, unused -- it only caps how many workgroups a CU holds (the
+    // probe's few registers would otherwise keep more waves in flight than any kernel it bounds)
     if (per_lane > 1)
-        hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(256), 0, st,
-                           q, ldr, out, ldr, n, tl);
+        hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(256),
+                           (size_t)lds, st, q, ldr, out, ldr, n, tl);
     else
-        hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(256), 0, st, q, ldr, out, ldr, n, tl);
+        hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(256), (size_t)lds, st, q, ldr, out, ldr, n, tl);
     return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
@@ -103,14 +106,25 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
 
 // rows_in / rows_out: (8, 60) FK + 6x8 J + pose (k_fk), (8, 126) 14 sphere distances + gradients
 // (k_coll, soffset-addressed outputs).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
-// per_lane > 1: the grid-strided form with that many units per workgroup.
+// per_lane > 1: the grid-strided form with that many units per workgroup.  lds: dynamic LDS bytes per
+// workgroup (0..65536) to cap the waves in flight per CU.
+extern "C" __attribute__((visibility("default"))) int kinprobe_pattern3(int rows_in, int rows_out, int64_t n,
+                                                                        int64_t tile, int64_t ld, int per_lane,
+                                                                        int lds, const float* q, float* out,
+                                                                        void* stream) {
+    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1 ||
+        lds < 0 || lds > 65536)
+        return -1;
+    const hipStream_t st = (hipStream_t)stream;
+    if (rows_in == 8 && rows_out == 60)
+        return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, lds, st);
+    if (rows_in == 8 && rows_out == 126)
+        return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, lds, st);
+    return -2;
+}
+
 extern "C" __attribute__((visibility("default"))) int kinprobe_pattern2(int rows_in, int rows_out, int64_t n,
                                                                         int64_t tile, int64_t ld, int per_lane,
                                                                         const float* q, float* out, void* stream) {
-    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1)
-        return -1;
-    const hipStream_t st = (hipStream_t)stream;
-    if (rows_in == 8 && rows_out == 60) return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, st);
-    if (rows_in == 8 && rows_out == 126) return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, st);
-    return -2;
+    return kinprobe_pattern3(rows_in, rows_out, n, tile, ld, per_lane, 0, q, out, stream);
 }

@@ -4,7 +4,8 @@ The product library libkinhip.so never reads these variables (kinhip_internal.h 
 
     python tools/ab.py <workload> [--reps R] [SETTING ...]
       workload: ik (tools/ik_ab.py: config-4 IK), coll (tools/coll_spec_ab.py: config-5 k_coll legs),
-                fk (tools/fk_legs_ab.py: headline FK + J and config 2)
+                fk (tools/fk_legs_ab.py: headline FK + J and config 2), jl (tools/jl_layout_ab.py: FK + J at
+                ld = N, the Julia shim's layout)
       SETTING:  "NAME=VALUE[,NAME=VALUE...]" -- one run per setting; "base" = no knob
     e.g. python tools/ab.py ik base KINHIP_IK_TWO_PHASE=0 KINHIP_IK_GROUP=2,KINHIP_IK_TWO_PHASE=0
          python tools/ab.py coll base "KINHIP_JIT_DEFS=-DKINHIP_AABB_UNROLL=1" KINHIP_COLL_FAST_TRIG=0
@@ -19,7 +20,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SCRIPTS = {"ik": "ik_ab.py", "coll": "coll_spec_ab.py", "fk": "fk_legs_ab.py"}
+SCRIPTS = {"ik": "ik_ab.py", "coll": "coll_spec_ab.py", "fk": "fk_legs_ab.py", "jl": "jl_layout_ab.py"}
 
 
 def main(argv):
