@@ -76,6 +76,12 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const int v = ab_env_int("KINHIP_FK_PER_LANE", 0);
         return v >= 1 && v <= 64 ? v : 0;
     }();
+    // KINHIP_FK_LDS=<bytes> (A/B): dynamic LDS reserved per workgroup of the specialised kernels, which caps
+    // the workgroups a CU holds (160 KB of LDS per CU)
+    static const int fk_lds_env = [] {
+        const int v = ab_env_int("KINHIP_FK_LDS", -1);
+        return v >= 0 && v <= 65536 ? v : -1;
+    }();
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
@@ -96,7 +102,8 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
             void* args[] = {(void*)&qc, (void*)&ldq, (void*)&cc, (void*)&pc, (void*)&ldp, (void*)&jc, (void*)&ldj,
                             (void*)&tl};
             // (specialised kernels keep branch frames in registers: no dynamic LDS)
-            const hipError_t e = hipModuleLaunchKernel(jit, gx, 1, 1, block.x, 1, 1, 0, st, args, nullptr);
+            const unsigned lds = fk_lds_env >= 0 ? (unsigned)fk_lds_env : 0u;
+            const hipError_t e = hipModuleLaunchKernel(jit, gx, 1, 1, block.x, 1, 1, lds, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }

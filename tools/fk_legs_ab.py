@@ -17,7 +17,10 @@ six = [m.find_link(n) for n in ["l_gripper_finger_link", "r_gripper_finger_link"
                                 "shoulder_lift_link", "upperarm_roll_link"]]
 n = 1 << 20
 res = []
-for name, dt, links, jac, tile in (("fkjac32", torch.float32, [gl], True, 8192), ("fk6_64", torch.float64, six, False, 4096)):
+legs = [("fkjac32", torch.float32, [gl], True, 8192, n), ("fk6_64", torch.float64, six, False, 4096, n)]
+if os.environ.get("FK_BIG"):  # 4x and 16x the Infinity Cache
+    legs += [("fkjac32_2^22", torch.float32, [gl], True, 8192, 1 << 22), ("fkjac32_2^24", torch.float32, [gl], True, 8192, 1 << 24)]
+for name, dt, links, jac, tile, n in legs:
     plan = m.plan(arm, out_links=links, jac_link=gl if jac else None, dtype=dt).specialize(kinhip.KIN_SPEC_FK)
     Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, dtype=dt, device=dev)
     Qt = kinhip.tiled(Q, tile)
@@ -28,10 +31,13 @@ for name, dt, links, jac, tile in (("fkjac32", torch.float32, [gl], True, 8192),
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(30):
+    reps = 30 if n <= 1 << 20 else 10
+    for _ in range(reps):
         plan.run_tiled(Qt, n, P, J)
     e1.record()
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / 30 * 1e3
+    us = e0.elapsed_time(e1) / reps * 1e3
+    del Q, Qt, P, J
     res.append(f"{name}: {us:6.1f}us chk {float(P.double().sum()):.9e}")
-print("defs", os.environ.get("KINHIP_JIT_DEFS", "-"), " | ".join(res), flush=True)
+print("defs", os.environ.get("KINHIP_JIT_DEFS", "-"), "lds", os.environ.get("KINHIP_FK_LDS", "-"), " | ".join(res),
+      flush=True)
