@@ -37,7 +37,7 @@ for name, dt, links, jac, tile, n in legs:
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
-    del Q, Qt, P, J
     res.append(f"{name}: {us:6.1f}us chk {float(P.double().sum()):.9e}")
+    del Q, Qt, P, J
 print("defs", os.environ.get("KINHIP_JIT_DEFS", "-"), "lds", os.environ.get("KINHIP_FK_LDS", "-"), " | ".join(res),
       flush=True)
