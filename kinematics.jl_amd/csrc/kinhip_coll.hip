@@ -33,6 +33,16 @@ __global__ __launch_bounds__(256) void k_coll_scene(const KProg<T> P, const KSte
 
 }  // namespace
 
+// KINHIP_COLL_LDS=<bytes> (A/B): reserve at least this much LDS per workgroup of the specialised
+// collision kernels (an occupancy cap, as launch_fk's)
+inline size_t coll_lds(size_t lds) {
+    static const int env = [] {
+        const int v = ab_env_int("KINHIP_COLL_LDS", -1);
+        return v >= 0 && v <= 65536 ? v : -1;
+    }();
+    return env >= 0 && (size_t)env > lds ? (size_t)env : lds;
+}
+
 template <typename T>
 hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                              const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
@@ -65,7 +75,7 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc, (void*)&ldd,
                             (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tc, (void*)&sa};
             const hipError_t e = hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1,
-                                                       (unsigned)lds, st, args, nullptr);
+                                                       (unsigned)coll_lds(lds), st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }
@@ -111,7 +121,8 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc,
                             (void*)&ldd, (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tl};
             const hipError_t e =
-                hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, (unsigned)lds, st, args, nullptr);
+                hipModuleLaunchKernel(jf->coll[grads ? 1 : 0], grid.x, 1, 1, 256, 1, 1, (unsigned)coll_lds(lds), st,
+                                      args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }

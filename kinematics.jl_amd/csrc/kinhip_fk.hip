@@ -76,8 +76,14 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const int v = ab_env_int("KINHIP_FK_PER_LANE", 0);
         return v >= 1 && v <= 64 ? v : 0;
     }();
-    // KINHIP_FK_LDS=<bytes> (A/B): dynamic LDS reserved per workgroup of the specialised kernels, which caps
-    // the workgroups a CU holds (160 KB of LDS per CU)
+    // Occupancy: the specialised one-configuration-per-lane kernel reserves 64 KB of (unused) LDS per
+    // 256-lane workgroup, so a CU holds 2 workgroups (8 waves, 2 per SIMD; 160 KB of LDS per CU): with fewer
+    // lanes streaming 8 rows in and 60 out at once, HBM serves them faster -- 2^20 FK + J 41.5 -> 40.6 us,
+    // 2^22 161 -> 153.5 us, fp64 6-link FK 107.5 -> 100.2 us; the grid-strided kernel (2^23+) keeps its
+    // full occupancy (730 vs 746 us capped), as does the pattern probe's own sweep (bench.py PROBE_LDS,
+    // profiles/r04_fk_occupancy_ab.txt, r04_ik_solve_probe_occ_ab.txt).
+    // KINHIP_FK_LDS=<bytes> (A/B) overrides the reservation of both specialised kernels.
+    constexpr unsigned kFkLds = 65536;
     static const int fk_lds_env = [] {
         const int v = ab_env_int("KINHIP_FK_LDS", -1);
         return v >= 0 && v <= 65536 ? v : -1;
@@ -102,7 +108,7 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
             void* args[] = {(void*)&qc, (void*)&ldq, (void*)&cc, (void*)&pc, (void*)&ldp, (void*)&jc, (void*)&ldj,
                             (void*)&tl};
             // (specialised kernels keep branch frames in registers: no dynamic LDS)
-            const unsigned lds = fk_lds_env >= 0 ? (unsigned)fk_lds_env : 0u;
+            const unsigned lds = fk_lds_env >= 0 ? (unsigned)fk_lds_env : jit == jf->fk ? kFkLds : 0u;
             const hipError_t e = hipModuleLaunchKernel(jit, gx, 1, 1, block.x, 1, 1, lds, st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;

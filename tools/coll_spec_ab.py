@@ -20,9 +20,17 @@ cp = sscc.plan(arm, dtype=dt).specialize()
 n = 1 << 20
 Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=555, dtype=dt,
                            device=dev)
+# the bench's f2 door sweep: boxes attached to the fridge, one door angle per sample
+asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+g = torch.Generator().manual_seed(90)
+SQ = torch.zeros((4, n), dtype=torch.float64)
+SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
+SQ[1] = 1.2
+SQ = SQ.to(dt).to(dev).contiguous()
 res = []
 for name, run in (("min", lambda: cp.run(sdf, Q, dists=False, min_dist=True)),
-                  ("grad", lambda: cp.run(sdf, Q, dists=True, grads=True))):
+                  ("grad", lambda: cp.run(sdf, Q, dists=True, grads=True)),
+                  ("scene", lambda: cp.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ))):
     for _ in range(3):
         r = run()
     torch.cuda.synchronize()
