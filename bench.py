@@ -558,31 +558,32 @@ def _pmc_traffic(workload, fname="pmc_fk_jac_f32.json"):
 _PROBE = None
 
 
-# dynamic LDS per 256-lane workgroup for the probe's occupancy sweep: 0 (as many waves as registers allow),
-# then 5, 4, 3, 2 and 1 workgroups per CU (160 KB of LDS per CU)
-PROBE_LDS = (0, 32768, 40960, 53248, 65536)
+# the probe's occupancy sweep: (dynamic LDS bytes, lanes) per workgroup -- as many waves as registers allow,
+# then 20, 16, 12, 8, 6 and 4 waves per CU (160 KB of LDS per CU)
+PROBE_OCC = ((0, 256), (32768, 256), (40960, 256), (53248, 256), (65536, 256), (53248, 128), (65536, 128))
 
 
 def _pattern_us(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0, per_lane=1):
-    """The fastest of the access pattern's runs over PROBE_LDS occupancies (_pattern_at)."""
-    return min(_pattern_at(rows_in, rows_out, n, tile, stream, reps, warmup, ld, per_lane, lds) for lds in PROBE_LDS)
+    """The fastest of the access pattern's runs over the PROBE_OCC occupancies (_pattern_at)."""
+    return min(_pattern_at(rows_in, rows_out, n, tile, stream, reps, warmup, ld, per_lane, lds, blk)
+               for lds, blk in PROBE_OCC)
 
 
-def _pattern_at(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0, per_lane=1, lds=0):
+def _pattern_at(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0, per_lane=1, lds=0, blk=256):
     """The access pattern of a leg with no arithmetic (kinematics.jl_amd/lib/libkinprobe.so, a measurement
     probe built beside the engine): rows_in rows of q read and rows_out rows written per configuration,
     fp32, tiled SoA (tile > 0) or plain rows (tile = 0) `ld` >= n elements apart (0: ld = n), addressed as
     the kernels address them (per-row buffer descriptors, 32-bit lane offsets, uniform tile divide,
     non-temporal stores; per_lane > 1: launch_fk's grid-strided form), `lds` bytes of unused LDS per
-    workgroup capping its occupancy.  Average launch time (µs) from HIP events on `stream`: the leg's
+    workgroup of `blk` lanes capping its occupancy.  Average launch time (µs) from HIP events on `stream`: the leg's
     ceiling measured in the same run."""
     global _PROBE
     import ctypes as C
     if _PROBE is None:
         _PROBE = C.CDLL(os.path.join(ROOT, "kinematics.jl_amd", "lib", "libkinprobe.so"))
-        _PROBE.kinprobe_pattern3.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
-                                             C.c_void_p, C.c_void_p, C.c_void_p]
-        _PROBE.kinprobe_pattern3.restype = C.c_int
+        _PROBE.kinprobe_pattern4.argtypes = [C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                             C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        _PROBE.kinprobe_pattern4.restype = C.c_int
     ld = tile if tile else (ld or n)
     ntot = -(-n // tile) * tile if tile else ld
     q = torch.zeros(rows_in * ntot, dtype=torch.float32, device=stream.device)
@@ -590,7 +591,8 @@ def _pattern_at(rows_in, rows_out, n, tile, stream, reps=20, warmup=3, ld=0, per
     st = stream.cuda_stream
 
     def launch():
-        rc = _PROBE.kinprobe_pattern3(rows_in, rows_out, n, tile, ld, per_lane, lds, q.data_ptr(), out.data_ptr(), st)
+        rc = _PROBE.kinprobe_pattern4(rows_in, rows_out, n, tile, ld, per_lane, lds, blk, q.data_ptr(), out.data_ptr(),
+                                      st)
         assert rc == 0, rc
     for _ in range(warmup):
         launch()
@@ -752,7 +754,7 @@ def main():
         pat = _pattern_us(8, 60, N, args.tile if args.layout == "tiled" else 0, stream, ld=N + args.row_pad)
         out["roofline"]["pattern_ceiling"] = {"avg_launch_us": pat, "frac_of_pattern": pat / (t_launch * 1e6),
                                               "achieved_GBs": bytes_per_eval * N / pat / 1e3,
-                                              "probe": "kinprobe_pattern3(8 in, 60 out, same layout and addressing), fastest over occupancies, same run"}
+                                              "probe": "kinprobe_pattern4(8 in, 60 out, same layout and addressing), fastest over occupancies, same run"}
         # The 2^20 working set (q + outputs, 285 MB) is about the 256 MiB Infinity Cache, so back-to-back
         # launches find part of the previous launch's lines on die.  Two checks beside the headline:
         # the same launch after a 1 GiB read has evicted the cache (cold), and batches 4x and 16x the

@@ -88,13 +88,19 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const int v = ab_env_int("KINHIP_FK_LDS", -1);
         return v >= 0 && v <= 65536 ? v : -1;
     }();
+    // KINHIP_FK_BLOCK=<64|128|256> (A/B): lanes per workgroup of the specialised kernels
+    static const int fk_block_env = [] {
+        const int v = ab_env_int("KINHIP_FK_BLOCK", 0);
+        return v == 64 || v == 128 || v == 256 ? v : 0;
+    }();
+    const int blk = jf && jf->fk && fk_block_env && ta.tile % fk_block_env == 0 ? fk_block_env : g.block;
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
-    Tiling tl{tiled ? (uint32_t)(ta.tile / g.block) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, 0};
+    Tiling tl{tiled ? (uint32_t)(ta.tile / blk) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, 0};
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         const int64_t c = std::min(chunk, n - s0);
-        const dim3 grid(grid_of(c, g.block)), block(g.block);
+        const dim3 grid(grid_of(c, blk)), block(blk);
         const int64_t tq = tiled ? (s0 / ta.tile) * ta.tsq : s0, tp = tiled ? (s0 / ta.tile) * ta.tsp : s0,
                       tj = tiled ? (s0 / ta.tile) * ta.tsj : s0;
         const T* qc = q ? q + tq : q;

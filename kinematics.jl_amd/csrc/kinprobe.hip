@@ -3,7 +3,7 @@
 // same run ("frac_of_pattern" = probe time / kernel time).  The probe addresses memory exactly as the
 // kernels do (kinhip_device.h, kinhip_fk_dev.h): one buffer descriptor per row (ld_soa / st_soa; the
 // collision kernels' soffset form sto_soa for their outputs), a 32-bit lane byte offset, the tile of a
-// workgroup from a uniform 32-bit divide (Tiling::tile_blocks), 256-lane workgroups, non-temporal
+// workgroup from a uniform 32-bit divide (Tiling::tile_blocks), 256-lane workgroups (or 128 / 64), non-temporal
 // stores, compile-time row counts, and -- for batches of 2^23 and more, like launch_fk's specialised
 // kernel -- the grid-strided form with the next unit's loads issued before this unit's stores.
 // Element (config i, row r) lives at (i / tile) * rows * tile + r * tile + i % tile (tiled SoA,
@@ -41,12 +41,12 @@ __device__ __forceinline__ void probe_store(float* __restrict__ out, int64_t ldo
 template <int RI, int RO, bool SOFF>
 __global__ __launch_bounds__(256) void p_pattern(const float* __restrict__ q, int64_t ldq, float* __restrict__ out,
                                                  int64_t ldo, int64_t n, Tiling tl) {
-    const uint32_t b = blockIdx.x, tid = threadIdx.x;
-    if ((uint64_t)b * 256u + tid >= (uint64_t)n) return;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, B = blockDim.x;
+    if ((uint64_t)b * B + tid >= (uint64_t)n) return;
     const uint32_t t = b / tl.tile_blocks;
     q += (int64_t)t * tl.tsq;
     out += (int64_t)t * tl.tsp;
-    const uint32_t off = ((b - t * tl.tile_blocks) * 256u + tid) * 4u;
+    const uint32_t off = ((b - t * tl.tile_blocks) * B + tid) * 4u;
     probe_store<RO, SOFF>(out, ldo, off, probe_load<RI>(q, ldq, off));
 }
 
@@ -54,50 +54,50 @@ __global__ __launch_bounds__(256) void p_pattern(const float* __restrict__ q, in
 template <int RI, int RO, bool SOFF>
 __global__ __launch_bounds__(256) void p_pattern_strided(const float* __restrict__ q, int64_t ldq,
                                                          float* __restrict__ out, int64_t ldo, int64_t n, Tiling tl) {
-    const uint32_t tid = threadIdx.x, units = (uint32_t)((n + 255) / 256);
+    const uint32_t tid = threadIdx.x, B = blockDim.x, units = (uint32_t)((n + B - 1) / B);
     uint32_t b = blockIdx.x;
     if (b >= units) return;
     auto addr = [&](uint32_t u, const float*& qb, float*& ob) {
         const uint32_t t = u / tl.tile_blocks;
         qb = q + (int64_t)t * tl.tsq;
         ob = out + (int64_t)t * tl.tsp;
-        return ((u - t * tl.tile_blocks) * 256u + tid) * 4u;
+        return ((u - t * tl.tile_blocks) * B + tid) * 4u;
     };
     const float* qb;
     float* ob;
     uint32_t off = addr(b, qb, ob);
-    float a = (uint64_t)b * 256u + tid < (uint64_t)n ? probe_load<RI>(qb, ldq, off) : 0.0f;
+    float a = (uint64_t)b * B + tid < (uint64_t)n ? probe_load<RI>(qb, ldq, off) : 0.0f;
     for (;;) {
         const uint32_t bn = b + gridDim.x;
         const bool more = bn < units;
         const float* qn;
         float* on;
         const uint32_t offn = more ? addr(bn, qn, on) : 0u;
-        const float an = more && (uint64_t)bn * 256u + tid < (uint64_t)n ? probe_load<RI>(qn, ldq, offn) : 0.0f;
-        if ((uint64_t)b * 256u + tid < (uint64_t)n) probe_store<RO, SOFF>(ob, ldo, off, a);
+        const float an = more && (uint64_t)bn * B + tid < (uint64_t)n ? probe_load<RI>(qn, ldq, offn) : 0.0f;
+        if ((uint64_t)b * B + tid < (uint64_t)n) probe_store<RO, SOFF>(ob, ldo, off, a);
         if (!more) break;
         b = bn; off = offn; ob = on; a = an;
     }
 }
 
 template <int RI, int RO, bool SOFF>
-int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, int lds,
+int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, int lds, int blk,
                    hipStream_t st) {
     const bool tiled = tile > 0;
-    if (tiled && tile % 256) return -1;
+    if (tiled && tile % blk) return -1;
     // tiled arrays: (ntiles, rows, tile) -- a tile of q is RI rows, a tile of out RO rows
-    Tiling tl{tiled ? (uint32_t)(tile / 256) : 0xffffffffu, tiled ? RI * tile : 0, tiled ? RO * tile : 0, 0, 0};
+    Tiling tl{tiled ? (uint32_t)(tile / blk) : 0xffffffffu, tiled ? RI * tile : 0, tiled ? RO * tile : 0, 0, 0};
     const int64_t ldr = tiled ? tile : ld;
     if ((uint64_t)(tiled ? tile : n) * 4u >= (1ull << 31)) return -1;  // 32-bit lane offsets
     if (SOFF && (uint64_t)(RO * ldr + (tiled ? tile : n)) * 4u >= (1ull << 31)) return -1;
-    const unsigned units = (unsigned)((n + 255) / 256);
+    const unsigned units = (unsigned)((n + blk - 1) / blk);
     // lds: dynamic LDS bytes per workgroup, unused -- it only caps how many workgroups a CU holds (the
     // probe's few registers would otherwise keep more waves in flight than any kernel it bounds)
     if (per_lane > 1)
-        hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(256),
+        hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(blk),
                            (size_t)lds, st, q, ldr, out, ldr, n, tl);
     else
-        hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(256), (size_t)lds, st, q, ldr, out, ldr, n, tl);
+        hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(blk), (size_t)lds, st, q, ldr, out, ldr, n, tl);
     return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
@@ -107,24 +107,25 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
 // rows_in / rows_out: (8, 60) FK + 6x8 J + pose (k_fk), (8, 126) 14 sphere distances + gradients
 // (k_coll, soffset-addressed outputs).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
 // per_lane > 1: the grid-strided form with that many units per workgroup.  lds: dynamic LDS bytes per
-// workgroup (0..65536) to cap the waves in flight per CU.
+// workgroup (0..65536) to cap the waves in flight per CU; blk: lanes per workgroup (64..256, a power of 2).
+extern "C" __attribute__((visibility("default"))) int kinprobe_pattern4(int rows_in, int rows_out, int64_t n,
+                                                                        int64_t tile, int64_t ld, int per_lane,
+                                                                        int lds, int blk, const float* q, float* out,
+                                                                        void* stream) {
+    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1 ||
+        lds < 0 || lds > 65536 || (blk != 64 && blk != 128 && blk != 256))
+        return -1;
+    const hipStream_t st = (hipStream_t)stream;
+    if (rows_in == 8 && rows_out == 60)
+        return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, lds, blk, st);
+    if (rows_in == 8 && rows_out == 126)
+        return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, lds, blk, st);
+    return -2;
+}
+
 extern "C" __attribute__((visibility("default"))) int kinprobe_pattern3(int rows_in, int rows_out, int64_t n,
                                                                         int64_t tile, int64_t ld, int per_lane,
                                                                         int lds, const float* q, float* out,
                                                                         void* stream) {
-    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1 ||
-        lds < 0 || lds > 65536)
-        return -1;
-    const hipStream_t st = (hipStream_t)stream;
-    if (rows_in == 8 && rows_out == 60)
-        return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, lds, st);
-    if (rows_in == 8 && rows_out == 126)
-        return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, lds, st);
-    return -2;
-}
-
-extern "C" __attribute__((visibility("default"))) int kinprobe_pattern2(int rows_in, int rows_out, int64_t n,
-                                                                        int64_t tile, int64_t ld, int per_lane,
-                                                                        const float* q, float* out, void* stream) {
-    return kinprobe_pattern3(rows_in, rows_out, n, tile, ld, per_lane, 0, q, out, stream);
+    return kinprobe_pattern4(rows_in, rows_out, n, tile, ld, per_lane, lds, 256, q, out, stream);
 }

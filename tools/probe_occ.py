@@ -14,5 +14,5 @@ st = torch.cuda.Stream(dev)
 for name, n, tile, ld, pl in (("2^20 tiled", 1 << 20, 8192, 0, 1), ("2^20 ld=N+256", 1 << 20, 0, (1 << 20) + 256, 1),
                               ("2^20 ld=N", 1 << 20, 0, 1 << 20, 1), ("2^22 tiled", 1 << 22, 8192, 0, 1),
                               ("2^24 tiled strided", 1 << 24, 8192, 0, 2)):
-    r = [bench._pattern_at(8, 60, n, tile, st, 10, 2, ld, pl, lds) for lds in bench.PROBE_LDS]
-    print(name, " ".join(f"lds{l}:{t:.1f}us" for l, t in zip(bench.PROBE_LDS, r)), flush=True)
+    r = [bench._pattern_at(8, 60, n, tile, st, 10, 2, ld, pl, lds, blk) for lds, blk in bench.PROBE_OCC]
+    print(name, " ".join(f"{l}/{b}:{t:.1f}us" for (l, b), t in zip(bench.PROBE_OCC, r)), flush=True)
