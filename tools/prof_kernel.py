@@ -163,6 +163,6 @@ else:
     tgt = T[0].contiguous()
     for _ in range(a.steps):
         Q0 = torch.zeros_like(Q)
-        plan.ik_dls(tgt, Q0, max_iters=64, restarts=3, lam=1e-2, max_step=1.0, damp_err=0.01)  # bench IK_KW
+        plan.ik_dls(tgt, Q0, max_iters=64, restarts=3, lam=1e-2, max_step=0.5)  # bench IK_KW
 torch.cuda.synchronize()
 print("done", a.what, a.steps)
