@@ -88,12 +88,16 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const int v = ab_env_int("KINHIP_FK_LDS", -1);
         return v >= 0 && v <= 65536 ? v : -1;
     }();
-    // KINHIP_FK_BLOCK=<64|128|256> (A/B): lanes per workgroup of the specialised kernels
+    // fp64: 128-lane workgroups for the one-per-lane specialised kernel (with the 64 KB reservation: 4 waves
+    // per CU, 1 per SIMD): config 2's fp64 FK of 6 links 101-104 -> 94 us; fp32 keeps 256 (44 us at 128)
+    // (profiles/r04_fk_block_probe_ab.txt).  KINHIP_FK_BLOCK=<64|128|256> (A/B) overrides.
     static const int fk_block_env = [] {
         const int v = ab_env_int("KINHIP_FK_BLOCK", 0);
         return v == 64 || v == 128 || v == 256 ? v : 0;
     }();
-    const int blk = jf && jf->fk && fk_block_env && ta.tile % fk_block_env == 0 ? fk_block_env : g.block;
+    const bool one_per_lane = !(per_lane_env > 1 || (n >= kFkStrideMin && jf && jf->fk_stride && !per_lane_env));
+    const int want = fk_block_env ? fk_block_env : (sizeof(T) == 8 && one_per_lane ? 128 : g.block);
+    const int blk = jf && jf->fk && (ta.tile >= n || ta.tile % want == 0) ? want : g.block;  // (tiles: whole blocks)
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
