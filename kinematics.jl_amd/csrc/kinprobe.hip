@@ -16,6 +16,7 @@
 
 namespace kinhip {
 namespace {
+typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
 
 template <int RI>
 __device__ __forceinline__ float probe_load(const float* __restrict__ q, int64_t ldq, uint32_t off) {
@@ -80,6 +81,39 @@ __global__ __launch_bounds__(256) void p_pattern_strided(const float* __restrict
     }
 }
 
+// the same bytes with the outputs staged through LDS: each lane writes its RO values into an [RO][B] LDS
+// block, then every wave writes whole rows, 16 bytes per lane (buffer_store_dwordx4: one instruction
+// covers 4 x 64 consecutive configurations of a row instead of 64) -- what an LDS-staged store path in
+// k_fk would emit.  Rows must be 16-byte aligned (ld % 4 == 0, tile % 4 == 0).
+template <int RI, int RO>
+__global__ __launch_bounds__(256) void p_pattern_x4(const float* __restrict__ q, int64_t ldq, float* __restrict__ out,
+                                                    int64_t ldo, int64_t n, Tiling tl) {
+    extern __shared__ float stage[];  // [RO][B]
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, B = blockDim.x;
+    const uint32_t t = b / tl.tile_blocks;
+    q += (int64_t)t * tl.tsq;
+    out += (int64_t)t * tl.tsp;
+    const uint32_t i0 = (b - t * tl.tile_blocks) * B;  // first configuration of the block (in its tile)
+    const bool valid = (uint64_t)b * B + tid < (uint64_t)n;
+    const float a = valid ? probe_load<RI>(q, ldq, (i0 + tid) * 4u) : 0.0f;
+#pragma unroll
+    for (int r = 0; r < RO; ++r) stage[r * B + tid] = a + (float)r;
+    __syncthreads();
+    const uint32_t w = tid >> 6, l = tid & 63u, nw = B >> 6, per_row = B / 4;  // lanes per row (16 B each)
+    const uint64_t left = (uint64_t)n - (uint64_t)b * B;                      // configurations of this block
+    for (uint32_t k = w * 64 + l; k < RO * per_row; k += nw * 64) {
+        const uint32_t r = k / per_row, c = (k - r * per_row) * 4;
+        if (c + 4 <= left) {
+            const float4 v = *reinterpret_cast<const float4*>(&stage[r * B + c]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), row_rsrc(out + r * ldo),
+                                                   (int)((i0 + c) * 4u), 0, KINHIP_STORE_AUX);
+        } else {
+            for (uint32_t e = c; e < B && e < left; ++e)
+                st_soa(out, r, ldo, (i0 + e) * 4u, stage[r * B + e]);
+        }
+    }
+}
+
 template <int RI, int RO, bool SOFF>
 int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* out, int per_lane, int lds, int blk,
                    hipStream_t st) {
@@ -96,7 +130,12 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
     if (per_lane > 1)
         hipLaunchKernelGGL((p_pattern_strided<RI, RO, SOFF>), dim3((units + per_lane - 1) / per_lane), dim3(blk),
                            (size_t)lds, st, q, ldr, out, ldr, n, tl);
-    else
+    else if (per_lane < 0) {  // (-1: the LDS-staged 16-byte row stores; lds is the staging block, at least RO * blk * 4)
+        if (SOFF || ldr % 4 || (size_t)RO * blk * 4 > 65536) return -1;
+        const size_t need = (size_t)RO * blk * 4;
+        hipLaunchKernelGGL((p_pattern_x4<RI, RO>), dim3(units), dim3(blk), (size_t)lds > need ? (size_t)lds : need, st,
+                           q, ldr, out, ldr, n, tl);
+    } else
         hipLaunchKernelGGL((p_pattern<RI, RO, SOFF>), dim3(units), dim3(blk), (size_t)lds, st, q, ldr, out, ldr, n, tl);
     return hipGetLastError() == hipSuccess ? 0 : -4;
 }
@@ -106,13 +145,14 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
 
 // rows_in / rows_out: (8, 60) FK + 6x8 J + pose (k_fk), (8, 126) 14 sphere distances + gradients
 // (k_coll, soffset-addressed outputs).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
-// per_lane > 1: the grid-strided form with that many units per workgroup.  lds: dynamic LDS bytes per
+// per_lane > 1: the grid-strided form with that many units per workgroup; -1: the LDS-staged 16-byte row stores
+// (p_pattern_x4, a layout experiment for k_fk).  lds: dynamic LDS bytes per
 // workgroup (0..65536) to cap the waves in flight per CU; blk: lanes per workgroup (64..256, a power of 2).
 extern "C" __attribute__((visibility("default"))) int kinprobe_pattern4(int rows_in, int rows_out, int64_t n,
                                                                         int64_t tile, int64_t ld, int per_lane,
                                                                         int lds, int blk, const float* q, float* out,
                                                                         void* stream) {
-    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < 1 ||
+    if (n <= 0 || n >= (int64_t(1) << 30) || tile < 0 || (tile > 0 ? ld != tile : ld < n) || per_lane < -1 || per_lane == 0 ||
         lds < 0 || lds > 65536 || (blk != 64 && blk != 128 && blk != 256))
         return -1;
     const hipStream_t st = (hipStream_t)stream;

@@ -16,3 +16,7 @@ for name, n, tile, ld, pl in (("2^20 tiled", 1 << 20, 8192, 0, 1), ("2^20 ld=N+2
                               ("2^24 tiled strided", 1 << 24, 8192, 0, 2)):
     r = [bench._pattern_at(8, 60, n, tile, st, 10, 2, ld, pl, lds, blk) for lds, blk in bench.PROBE_OCC]
     print(name, " ".join(f"{l}/{b}:{t:.1f}us" for (l, b), t in zip(bench.PROBE_OCC, r)), flush=True)
+    if pl == 1:  # the LDS-staged 16-byte row stores (p_pattern_x4)
+        occ = ((61440, 256), (65536, 256), (30720, 128), (53248, 128), (65536, 128))
+        r = [bench._pattern_at(8, 60, n, tile, st, 10, 2, ld, -1, lds, blk) for lds, blk in occ]
+        print(name, "x4", " ".join(f"{l}/{b}:{t:.1f}us" for (l, b), t in zip(occ, r)), flush=True)
