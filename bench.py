@@ -851,7 +851,10 @@ def main():
         out["config4_ik_dls"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec)
         out["config4_ik_dls"]["pmc"] = _pmc_valu("pmc_ik32s.json")
         # the reference's own objective (src/inverse_kinematics.jl:38-50: [p* - p; rpy* - rpy], rpy_jac)
-        out["config4_ik_dls_rpy"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, over=dict(with_rot=2))
+        # (with the error-scaled damping: the rpy residual converges worse on a fixed lambda -- 0.992 success
+        # at max_step 0.5, 0.997 damped, profiles/r04_bench_k.json)
+        out["config4_ik_dls_rpy"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec,
+                                            over=dict(IK_KW_DAMPED, with_rot=2))
         # the error-scaled damping (kin_ik_params.damp_err) for comparison
         out["config4_ik_dls_damped"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec,
                                                over=dict(max_step=1.0, damp_err=0.01))
