@@ -241,3 +241,39 @@ def test_ik_iters_contract(fetch):
     _, it3, err3 = m.ik_dls_batch(np.zeros((8, 1)), ids, gl, tgt, max_iters=k - 1, tol_pos=1e-4, tol_rot=1e-4)
     assert int(it3[0]) == k  # (k - 1) + 1: not converged
     assert not (err3[0, 0] < 1e-4 and err3[1, 0] < 1e-4)
+
+
+@pytest.mark.parametrize("damp_err", [0.0, 0.01, 0.3])
+def test_ik_damped_step_restated(fetch, damp_err):
+    """One step of the oracle's DLS IK (or_ik_dls_batch) against its statement written out in numpy:
+    dq = J^T (J J^T + (lambda^2 + damp_err (|dp|^2 + |rot|^2)) I)^-1 e with e = [p* - p; log(R* R^T)],
+    |dq|_inf clamped to max_step, q clamped to the limits -- the error-scaled damping of
+    kin_ik_params.damp_err included (from inside the limits: no joint is held)."""
+    m = O.OracleMech(fetch)
+    ids = [fetch.joint_id(n) for n in ARM]
+    gl = fetch.link_id("gripper_link")
+    rng = np.random.default_rng(3)
+    lo = np.array([fetch.joint_lower[j - 1] for j in ids], dtype=float)
+    hi = np.array([fetch.joint_upper[j - 1] for j in ids], dtype=float)
+    lo = np.where(np.isfinite(lo), lo, -np.pi)
+    hi = np.where(np.isfinite(hi), hi, np.pi)
+    N = 16
+    q0 = lo[:, None] + (hi - lo)[:, None] * (0.25 + 0.5 * rng.random((8, N)))
+    qt = lo[:, None] + (hi - lo)[:, None] * (0.25 + 0.5 * rng.random((8, N)))
+    tgt = m.fk_batch(qt, ids, [gl])[0]
+    lam, ms = 1e-2, 0.5
+    q1, _, _ = m.ik_dls_batch(q0, ids, gl, tgt, max_iters=1, lam=lam, max_step=ms, tol_pos=0.0, tol_rot=0.0,
+                              damp_err=damp_err)
+    pose, J = m.fk_jac_batch(q0, ids, gl, ids)
+    for i in range(N):
+        T = np.eye(4)
+        T[:3, :4] = tgt[:, i].reshape(4, 3).T
+        Tn = np.eye(4)
+        Tn[:3, :4] = pose[:, i].reshape(4, 3).T
+        e = np.concatenate([T[:3, 3] - Tn[:3, 3], O.rot_error(T, Tn)])
+        Ji = J[:, :, i].T  # [6, 8]
+        l2 = lam * lam + damp_err * (e[:3] @ e[:3] + e[3:] @ e[3:])
+        dq = Ji.T @ np.linalg.solve(Ji @ Ji.T + l2 * np.eye(6), e)
+        sc = min(1.0, ms / np.abs(dq).max())
+        ref = np.clip(q0[:, i] + sc * dq, lo, hi)
+        np.testing.assert_allclose(q1[:, i], ref, atol=1e-12)
