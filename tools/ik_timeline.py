@@ -20,7 +20,9 @@ Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j i
                             dtype=torch.float32, device=dev)
 tgt = plan.run(Qt)[0][0].contiguous()
 Q0 = torch.zeros((8, n), dtype=torch.float32, device=dev)
-kw = dict(max_iters=64, restarts=3, seed=0, lam=1e-2, max_step=0.5, tol_pos=1e-3, tol_rot=1e-3)
+kw = dict(max_iters=64, restarts=3, seed=0, lam=1e-2, max_step=float(os.environ.get("IK_MAXSTEP", 0.5)),
+          damp_err=float(os.environ.get("IK_DAMP", 0.0)), tol_pos=1e-3, tol_rot=1e-3)
+print(f"max_step {kw['max_step']} damp_err {kw['damp_err']}")
 Q = Q0.clone()
 for _ in range(5):
     _, it, err = plan.ik_dls(tgt, Q, Q0=Q0, **kw)
