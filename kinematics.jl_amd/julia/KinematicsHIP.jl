@@ -266,10 +266,11 @@ function get_jacobian_tiled!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, 
 end
 
 function Kinematics.get_jacobian(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot::Bool,
-                                 Q::ROCMatrix{T}; rpy_jac=false) where {T}
+                                 Q::DevMat{T}; rpy_jac=false) where {T}
     rows = with_rot ? 6 : 3
     cols = length(joints) + (hm.m.with_base ? 3 : 0)
-    J = AMDGPU.zeros(T, size(Q, 1), rows, cols)
+    J = batch_array(T, size(Q, 1), rows, cols)  # (padded rows, see batch_array)
+    fill!(J, zero(T))
     Kinematics.get_jacobian!(hm, link, joints, with_rot, J, Q; rpy_jac=rpy_jac)
 end
 
