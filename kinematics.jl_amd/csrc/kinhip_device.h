@@ -401,37 +401,16 @@ __device__ __forceinline__ void base_frame(Fr<T>& f, T bx, T by, T th) {  // src
 // Jacobian column = 6 or 3 rows) for this lane's configuration, one 4/8-byte
 // store per row.  (A 16-byte-per-lane variant staged through LDS measured 5%
 // slower: this stream runs at the ceiling of its access pattern, see
-// profiles/r01_store_probe.txt.)
-#ifndef KINHIP_FK_STAGE
-#define KINHIP_FK_STAGE 0  // 1 (specialised FK kernels, A/B): the LDS-staged row stores below (Tiling::stage)
-#endif
+// profiles/r01_store_probe.txt.  Round 4 again, with the occupancy cap: the
+// staged pattern probe 3-9% slower than this one, a staged k_fk 4x slower --
+// profiles/r04_fk_staged_stores_ab.txt; not kept.)
 template <typename T>
 struct Sink {
     uint32_t off;  // lane byte offset
-#if KINHIP_FK_STAGE
-    // staged: this lane's value of (array, row) goes to stage[srow * B + tid], srow = row (poses) or
-    // jrow0 + row (jac); the rows written are marked in m (uniform over the lanes that run)
-    T* stage = nullptr;
-    const T* pbase = nullptr;
-    uint32_t jrow0 = 0, tid = 0, B = 0;
-    mutable uint64_t m[2] = {0ull, 0ull};
-#endif
 
     template <int NR>
     __device__ __forceinline__ void rows(T* __restrict__ base, int64_t row0, int64_t ld, const T (&v)[NR],
                                          int nvalid) const {
-#if KINHIP_FK_STAGE
-        if (stage) {
-            const uint32_t r0 = (base == pbase ? 0u : jrow0) + (uint32_t)row0;
-#pragma unroll
-            for (int k = 0; k < NR; ++k)
-                if (k < nvalid) {
-                    stage[(r0 + k) * B + tid] = v[k];
-                    m[(r0 + k) >> 6] |= 1ull << ((r0 + k) & 63u);
-                }
-            return;
-        }
-#endif
 #pragma unroll
         for (int k = 0; k < NR; ++k)
             if (k < nvalid) st_soa(base, row0 + k, ld, off, v[k]);

@@ -102,14 +102,6 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
     const bool tiled = ta.tile < n;
     const int64_t chunk = tiled ? (kChunk / ta.tile) * ta.tile : kChunk;
     Tiling tl{tiled ? (uint32_t)(ta.tile / blk) : 0xffffffffu, ta.tsq, ta.tsp, ta.tsj, 0};
-    // KINHIP_FK_STAGE_ON=1 (A/B, with kernels built by KINHIP_JIT_DEFS=-DKINHIP_FK_STAGE=1): staged row stores
-    // (kinhip_fk_dev.h fk_stage_out) where the rows fit the 64 KB reservation
-    static const bool stage_env = ab_env_int("KINHIP_FK_STAGE_ON", 0) != 0;
-    const int64_t srows = g.pose_rows + g.jac_rows;
-    if (stage_env && jf && jf->fk && srows <= 128 && srows * blk * (int64_t)sizeof(T) <= 65536 - 16) {
-        tl.stage = 1;
-        tl.jrow0 = (uint32_t)g.pose_rows;
-    }
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         const int64_t c = std::min(chunk, n - s0);
         const dim3 grid(grid_of(c, blk)), block(blk);

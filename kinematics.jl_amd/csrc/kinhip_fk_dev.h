@@ -36,51 +36,7 @@ template <typename T, int MAXA>
 __device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __restrict__ S, T* slots,
                                        const T* __restrict__ q, int64_t ldq, T* __restrict__ poses, int64_t ldp,
                                        T* __restrict__ jac, int64_t ldj, const Tiling& tl, uint32_t b,
-                                       const T (&qa)[MAXA], const T (&bq)[3], T* stage = nullptr,
-                                       uint64_t* mask = nullptr);
-
-#if KINHIP_FK_STAGE
-// Staged stores (Tiling::stage, specialised kernels built with KINHIP_FK_STAGE): the lanes of a workgroup
-// write their outputs into LDS ([row][B], fk_one's Sink), then the workgroup writes every output row as
-// whole 16-byte runs per lane -- one buffer_store_dwordx4 covers 64 x 16 B of a row instead of 64 x 4 B.
-// The host reserves 64 KB of dynamic LDS (rows * B * sizeof(T) <= 65520; the last 16 bytes carry the
-// written-rows mask) and only stages when that fits; rows or bases that are not 16-byte aligned take
-// per-element stores from the staged copy.
-extern __shared__ __attribute__((aligned(16))) unsigned char kin_fk_stage[];
-template <typename T>
-__device__ __forceinline__ void fk_stage_out(const T* __restrict__ stage, uint64_t m0, uint64_t m1, uint32_t jrow0,
-                                             T* __restrict__ poses, int64_t ldp, T* __restrict__ jac, int64_t ldj,
-                                             uint32_t i0, uint64_t left) {
-    constexpr uint32_t per = 16u / (uint32_t)sizeof(T);  // values per 16-byte store
-    const uint32_t B = blockDim.x, tid = threadIdx.x, lanes_row = B / per, ngroups = B / lanes_row;
-    const uint32_t grp = tid / lanes_row, c = (tid - grp * lanes_row) * per;
-    const bool alp = poses && (reinterpret_cast<uint64_t>(poses) % 16u == 0) && ((ldp * (int64_t)sizeof(T)) % 16 == 0);
-    const bool alj = jac && (reinterpret_cast<uint64_t>(jac) % 16u == 0) && ((ldj * (int64_t)sizeof(T)) % 16 == 0);
-    uint32_t j = 0;
-    for (int h = 0; h < 2; ++h) {
-        uint64_t mm = h ? m1 : m0;
-        while (mm) {  // (uniform)
-            const uint32_t r = (uint32_t)__builtin_ctzll(mm) + 64u * (uint32_t)h;
-            mm &= mm - 1;
-            if (j++ % ngroups != grp) continue;  // (uniform inside a wave)
-            const bool isp = r < jrow0;
-            T* __restrict__ arr = isp ? poses : jac;
-            const int64_t rr = isp ? (int64_t)r : (int64_t)(r - jrow0), ld = isp ? ldp : ldj;
-            const T* src = stage + (size_t)r * B + c;
-            if ((isp ? alp : alj) && c + per <= left) {
-                typedef unsigned int u32x4_t __attribute__((__vector_size__(16)));
-                const u32x4_t v = *reinterpret_cast<const u32x4_t*>(src);
-                __builtin_amdgcn_raw_buffer_store_b128(v, row_rsrc(arr + rr * ld), (int)((i0 + c) * (uint32_t)sizeof(T)), 0,
-                                                       KINHIP_STORE_AUX);
-            } else {
-#pragma unroll
-                for (uint32_t e = 0; e < per; ++e)
-                    if (c + e < left) st_soa(arr, rr, ld, (i0 + c + e) * (uint32_t)sizeof(T), src[e]);
-            }
-        }
-    }
-}
-#endif
+                                       const T (&qa)[MAXA], const T (&bq)[3]);
 
 // STRIDE: grid-strided units with the next unit's angles prefetched (launch_fk picks it for batches
 // far larger than the Infinity Cache; specialised kernels only)
@@ -113,24 +69,6 @@ __device__ __forceinline__ void fk_body(const KProg<T>& P, const KStep<T>* __res
     }
     } else {
     const uint32_t b = config_block();
-#if KINHIP_FK_STAGE
-    if (tl.stage) {  // (uniform) every lane reaches the barrier; the lanes past n only skip their own work
-        T* stage = reinterpret_cast<T*>(kin_fk_stage);
-        uint64_t* mshare = reinterpret_cast<uint64_t*>(kin_fk_stage + 65536 - 16);
-        uint64_t mk[2] = {0ull, 0ull};
-        if ((uint64_t)b * B + tid < (uint64_t)n) {
-            fk_load<T, MAXA>(P, S, q, ldq, tl, b, qa, bq);
-            fk_one<T, MAXA>(P, S, slots, q, ldq, poses, ldp, jac, ldj, tl, b, qa, bq, stage, mk);
-        }
-        if (tid == 0) { mshare[0] = mk[0]; mshare[1] = mk[1]; }  // (lane 0 runs: its block exists for it)
-        __syncthreads();
-        const uint32_t t = b / tl.tile_blocks;
-        fk_stage_out<T>(stage, mshare[0], mshare[1], tl.jrow0, poses ? poses + (int64_t)t * tl.tsp : poses, ldp,
-                        jac ? jac + (int64_t)t * tl.tsj : jac, ldj, (b - t * tl.tile_blocks) * B,
-                        (uint64_t)n - (uint64_t)b * B);
-        return;
-    }
-#endif
     if ((uint64_t)b * B + tid >= (uint64_t)n) return;  // no block-wide barrier below: LDS slots are per lane
     fk_load<T, MAXA>(P, S, q, ldq, tl, b, qa, bq);
     fk_one<T, MAXA>(P, S, slots, q, ldq, poses, ldp, jac, ldj, tl, b, qa, bq);
@@ -142,7 +80,7 @@ template <typename T, int MAXA>
 __device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __restrict__ S, T* slots,
                                        const T* __restrict__ q, int64_t ldq, T* __restrict__ poses, int64_t ldp,
                                        T* __restrict__ jac, int64_t ldj, const Tiling& tl, uint32_t b,
-                                       const T (&qa)[MAXA], const T (&bq)[3], T* stage, uint64_t* mask) {
+                                       const T (&qa)[MAXA], const T (&bq)[3]) {
     const int B = blockDim.x, tid = threadIdx.x;
 #ifdef KINHIP_JIT
     // specialised kernels: every slot index is a constant, so branch frames live in registers
@@ -163,15 +101,6 @@ __device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __rest
     const uint32_t off = i * (uint32_t)sizeof(T);
     Sink<T> sk;
     sk.off = off;
-#if KINHIP_FK_STAGE
-    if (stage) {
-        sk.stage = stage;
-        sk.pbase = poses;
-        sk.jrow0 = tl.jrow0;
-        sk.tid = (uint32_t)tid;
-        sk.B = (uint32_t)B;
-    }
-#endif
 
     const bool base = (P.flags & PF_BASE) != 0;
     const T bx = bq[0], by = bq[1], bth = bq[2];
@@ -264,11 +193,6 @@ __device__ __forceinline__ void fk_one(const KProg<T>& P, const KStep<T>* __rest
         }
         if (st.save >= 0) KIN_SLOT_STORE(st.save, f);
     }
-#if KINHIP_FK_STAGE
-    if (mask) { mask[0] = sk.m[0]; mask[1] = sk.m[1]; }
-#else
-    (void)stage; (void)mask;
-#endif
 }
 
 #undef KIN_SLOT_STORE

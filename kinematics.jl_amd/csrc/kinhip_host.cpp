@@ -721,8 +721,6 @@ struct Stager {
         P.geom.block = block;
         P.geom.lds = (size_t)n_slots * 12 * block * esz;  // per-lane branch slots
         P.geom.maxA = nA;
-        P.geom.pose_rows = 12 * d.n_out;
-        P.geom.jac_rows = P.rows * P.ncols;
         auto fill = [&](auto& K, auto* host) {
             using T = std::remove_reference_t<decltype(host[0].F[0])>;
             K.nA = nA;

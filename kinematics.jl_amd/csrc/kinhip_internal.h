@@ -35,7 +35,6 @@ struct LaunchGeom {
     int block;      // threads per workgroup (multiple of 64)
     size_t lds;     // dynamic LDS bytes
     int maxA;       // phase-A steps as compiled (4 / 8 / 12 / 16 / 32); the program is padded to it
-    int pose_rows = 0, jac_rows = 0;  // output rows of a configuration: 12 per output link, rows x columns of J
 };
 
 // Tiled SoA (kin_plan_run_tiled): element (i, r) of an array at (i / tile) * ts + r * ld + i % tile.

@@ -179,9 +179,6 @@ struct Tiling {
     uint32_t tile_blocks;
     int64_t tsq, tsp, tsj;  // k_fk: q, poses, jac; k_coll: q, dists, grads
     int64_t tsm;            // k_coll: min_dist
-    // k_fk built with KINHIP_FK_STAGE: outputs staged through LDS and written as whole rows (stage = 1);
-    // jrow0 = the staged row of Jacobian row 0 (= the pose rows, 12 per output link)
-    uint32_t stage = 0, jrow0 = 0;
 };
 
 struct CollArgs {
