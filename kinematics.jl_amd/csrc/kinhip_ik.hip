@@ -224,6 +224,8 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a2.p1_cut = cut;
             a2.fail_aux = scr.fail_aux;
             a2.idx = scr.fail_list;
+            static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 1);  // (A/B: 0 = block-major waves)
+            a2.p2_spread = spread_env != 0 ? 1 : 0;
             a2.fail_ctl = scr.fail_ctl;
             a2.fail_mask = (uint32_t)(scr.ring_cap - 1);
             const int na2 = natt - a2.att0;

@@ -202,6 +202,9 @@ struct IkArgsT {
     int32_t* fail_aux;
     // error-scaled damping (kin_ik_params.damp_err): the solve's lambda^2 + damp_err (|dp|^2 + |rot|^2)
     T damp_err;
+    // phase 2: list entries go to the first wave of every workgroup, then the second, ... (1), so that a
+    // short list spreads over all CUs instead of filling the first workgroups' CUs two waves per SIMD
+    int32_t p2_spread;
 };
 
 // lambda^2 + mu (ep^2 + er^2) rounded operation by operation, as the oracle forms it (no contraction)
@@ -298,7 +301,8 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                                         int64_t chunk) {
     const int lane = (int)(threadIdx.x & 63u);
     const int slot = lane % G, grp = lane / G;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t wave = (a.idx && a.p2_spread) ? (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x
+                                                : ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     // two-phase control words (see IkArgsT): one lane per ring of the grid's first wave moves its start marks
     if (blockIdx.x == 0 && threadIdx.x < (unsigned)kIkSubRings && (a.phase1 || a.idx)) {
         uint32_t* c = a.fail_ctl + threadIdx.x * kIkCtlStride;
