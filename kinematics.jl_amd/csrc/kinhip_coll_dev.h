@@ -62,12 +62,13 @@ constexpr int kCollLdsBoxes = 64;
 // UnionSDF of NS points at once (NS = 2: two spheres of one link share every box's data, loaded
 // once through the scalar cache, and the loop overhead).  d[i] = sdf(p_i); GRAD: gw[i] = its
 // analytic gradient.
-template <typename T, bool GRAD, int NS>
-__device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
-                                          int nb, const T (&px)[NS], const T (&py)[NS], const T (&pz)[NS],
-                                          T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem, bool use_lds) {
-    T best[NS];
-    int bk[NS];
+// union_argmin: the surrogate minimum best[i] (and, ARG, the index bk[i] of its first box) over the
+// union; box_gradient: the analytic gradient of box k at p; union_sdf = both.
+template <typename T, bool ARG, int NS>
+__device__ __forceinline__ void union_argmin(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
+                                             int nb, const T (&px)[NS], const T (&py)[NS], const T (&pz)[NS],
+                                             T (&best)[NS], int (&bk)[NS]) {
+    constexpr bool GRAD = ARG;
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         best[i] = T(INFINITY);
@@ -120,51 +121,63 @@ __device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, con
             }
         }
     }
+}
+
+// analytic gradient of box k (a per-lane index) at p, in the box's own frame, rotated to the world
+template <typename T>
+__device__ __forceinline__ void box_gradient(const KBox<T>* __restrict__ boxes, const unsigned char* smem, bool use_lds,
+                                             int k, T px, T py, T pz, T (&gw)[3]) {
+    // explicit address spaces: the two gathers are ds_read and global_load, never one flat
+    // load through a selected pointer (which the optimiser otherwise forms from the branch)
+    KBox<T> b;
+    if (use_lds) {
+        const __attribute__((address_space(3))) KBox<T>* lb = (const __attribute__((address_space(3))) KBox<T>*)smem;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) b.inv[j] = lb[k].inv[j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) b.half[j] = lb[k].half[j];
+    } else {
+        const __attribute__((address_space(1))) KBox<T>* gb = (const __attribute__((address_space(1))) KBox<T>*)boxes;
+#pragma unroll
+        for (int j = 0; j < 12; ++j) b.inv[j] = gb[k].inv[j];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) b.half[j] = gb[k].half[j];
+    }
+    T l[3], q[3], gl[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        l[j] = fma(b.inv[4 * j], px, fma(b.inv[4 * j + 1], py, fma(b.inv[4 * j + 2], pz, b.inv[4 * j + 3])));
+        q[j] = fabs(l[j]) - b.half[j];
+    }
+    const T mx = fmax(q[0], fmax(q[1], q[2]));
+    if (mx > T(0)) {  // outside: d = |max(q, 0)|
+        const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
+        const T oo = o[0] * o[0] + o[1] * o[1] + o[2] * o[2];
+        T rn;  // fp32: hardware v_rsq_f32 (1 ulp) instead of the ~10-instruction IEEE division
+        if constexpr (sizeof(T) == 4) rn = rsqrt_fast(oo);
+        else rn = T(1) / sqrt_t(oo);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gl[j] = (l[j] < T(0) ? -o[j] : o[j]) * rn;
+    } else {  // inside: d = max(q)
+        const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) gl[j] = (j == im) ? (l[j] < T(0) ? T(-1) : T(1)) : T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) gw[j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
+}
+
+template <typename T, bool GRAD, int NS>
+__device__ __forceinline__ void union_sdf(const KBox<T>* __restrict__ boxes, const KAabb<T>* __restrict__ aabb, int na,
+                                          int nb, const T (&px)[NS], const T (&py)[NS], const T (&pz)[NS],
+                                          T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem, bool use_lds) {
+    T best[NS];
+    int bk[NS];
+    union_argmin<T, GRAD, NS>(boxes, aabb, na, nb, px, py, pz, best, bk);
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         d[i] = signed_sqrt(best[i]);
-        if (GRAD) {  // analytic gradient of the argmin box, in its own frame, rotated to the world
-            // explicit address spaces: the two gathers are ds_read and global_load, never one flat
-            // load through a selected pointer (which the optimiser otherwise forms from the branch)
-            KBox<T> b;
-            if (use_lds) {
-                const __attribute__((address_space(3))) KBox<T>* lb =
-                    (const __attribute__((address_space(3))) KBox<T>*)smem;
-#pragma unroll
-                for (int j = 0; j < 12; ++j) b.inv[j] = lb[bk[i]].inv[j];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) b.half[j] = lb[bk[i]].half[j];
-            } else {
-                const __attribute__((address_space(1))) KBox<T>* gb = (const __attribute__((address_space(1))) KBox<T>*)boxes;
-#pragma unroll
-                for (int j = 0; j < 12; ++j) b.inv[j] = gb[bk[i]].inv[j];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) b.half[j] = gb[bk[i]].half[j];
-            }
-            T l[3], q[3], gl[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                l[j] = fma(b.inv[4 * j], px[i], fma(b.inv[4 * j + 1], py[i], fma(b.inv[4 * j + 2], pz[i], b.inv[4 * j + 3])));
-                q[j] = fabs(l[j]) - b.half[j];
-            }
-            const T mx = fmax(q[0], fmax(q[1], q[2]));
-            if (mx > T(0)) {  // outside: d = |max(q, 0)|
-                const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
-                const T oo = o[0] * o[0] + o[1] * o[1] + o[2] * o[2];
-                T rn;  // fp32: hardware v_rsq_f32 (1 ulp) instead of the ~10-instruction IEEE division
-                if constexpr (sizeof(T) == 4) rn = rsqrt_fast(oo);
-                else rn = T(1) / sqrt_t(oo);
-#pragma unroll
-                for (int j = 0; j < 3; ++j) gl[j] = (l[j] < T(0) ? -o[j] : o[j]) * rn;
-            } else {  // inside: d = max(q)
-                const int im = (q[0] >= q[1] && q[0] >= q[2]) ? 0 : (q[1] >= q[2] ? 1 : 2);
-#pragma unroll
-                for (int j = 0; j < 3; ++j) gl[j] = (j == im) ? (l[j] < T(0) ? T(-1) : T(1)) : T(0);
-            }
-#pragma unroll
-            for (int j = 0; j < 3; ++j)
-                gw[i][j] = fma(b.inv[j], gl[0], fma(b.inv[4 + j], gl[1], b.inv[8 + j] * gl[2]));
-        }
+        if (GRAD) box_gradient<T>(boxes, smem, use_lds, bk[i], px[i], py[i], pz[i], gw[i]);
     }
 }
 
@@ -251,17 +264,20 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const K
                                             const KAabb<T>* __restrict__ aabb, const T (&px)[NS], const T (&py)[NS],
                                             const T (&pz)[NS], T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem,
                                             bool use_lds) {
+    int wg[NS], wk[NS];  // GRAD: the winning group (-1: none) and its argmin box (index into boxes)
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         d[i] = T(INFINITY);
         gw[i][0] = gw[i][1] = gw[i][2] = T(0);
+        wg[i] = -1;
+        wk[i] = 0;
     }
 #pragma unroll
     for (int g = 0; g < MAXG; ++g) {
         if (g >= sc.ng) break;  // uniform
         const KSceneGroup& G = sc.gr[g];
         const T* I = sc.inv[g];
-        T lx[NS], ly[NS], lz[NS], dg[NS], gg[NS][3];
+        T lx[NS], ly[NS], lz[NS];
         // Exact cull: every box of the group lies in its enclosing box (bc, bh), so the distance to that
         // box is a lower bound of the group's distance; a group that cannot come below the minimum of the
         // earlier groups (dg < d takes a group) is skipped -- with a slack beyond the rounding of both
@@ -282,17 +298,44 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const K
             need |= !(lb2 > lim * lim);
         }
         if (!need) continue;  // (per lane: a wave skips the group when none of its lanes needs it)
-        union_sdf<T, GRAD, NS>(boxes + G.box0, aabb + G.aabb0, G.na, G.nb, lx, ly, lz, dg, gg,
-                               smem + (size_t)G.box0 * sizeof(KBox<T>), use_lds);
+        T best[NS];
+        int bk[NS];
+        union_argmin<T, GRAD, NS>(boxes + G.box0, aabb + G.aabb0, G.na, G.nb, lx, ly, lz, best, bk);
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            if (dg[i] < d[i]) {
-                d[i] = dg[i];
-                if (GRAD) {  // world gradient = R_g g_local, R_g = (inverse rotation)^T
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) gw[i][j] = fma(I[j], gg[i][0], fma(I[4 + j], gg[i][1], I[8 + j] * gg[i][2]));
+            const T dg = signed_sqrt(best[i]);
+            if (dg < d[i]) {
+                d[i] = dg;
+                if (GRAD) {
+                    wg[i] = g;
+                    wk[i] = G.box0 + bk[i];
                 }
             }
+        }
+    }
+    if constexpr (GRAD) {
+        // the gradient once, of the winning group's argmin box (a group that does not win costs no
+        // gradient): the group frame selected per lane, the box-frame point recomputed exactly as the
+        // group loop formed it, and world gradient = R_g g_local, R_g = (inverse rotation)^T
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (wg[i] < 0) continue;  // no group below +inf (NaN input): a zero gradient
+            T I[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) I[j] = sc.inv[0][j];
+#pragma unroll
+            for (int g = 1; g < MAXG; ++g) {
+                if (g >= sc.ng) break;  // uniform
+#pragma unroll
+                for (int j = 0; j < 12; ++j) I[j] = wg[i] == g ? sc.inv[g][j] : I[j];
+            }
+            const T lx = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
+            const T ly = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
+            const T lz = fma(I[8], px[i], fma(I[9], py[i], fma(I[10], pz[i], I[11])));
+            T gg[3];
+            box_gradient<T>(boxes, smem, use_lds, wk[i], lx, ly, lz, gg);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) gw[i][j] = fma(I[j], gg[0], fma(I[4 + j], gg[1], I[8 + j] * gg[2]));
         }
     }
 }

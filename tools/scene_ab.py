@@ -1,0 +1,45 @@
+"""Door-sweep A/B (bench.py's f2 leg, specialised fp32): `blocks` timed blocks of 20 launches each,
+printing the median and minimum per-launch time and a checksum of the outputs (identical results across
+library builds show as equal checksums).  KINHIP_LIB selects the library.   python tools/scene_ab.py [blocks]"""
+import os
+import statistics
+import sys
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kinematics.jl_amd"))
+import kinhip  # noqa: E402
+
+dev = torch.device("cuda", 0)
+m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fetch.urdf"))
+fr = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "fridge.urdf"), with_base=True)
+sscc = kinhip.add_fetch_arm_spheres(kinhip.SweptSphereCollisionChecker(m))
+arm = [m.find_joint(n) for n in kinhip.FETCH_ARM_JOINTS]
+dt = torch.float32
+cp = sscc.plan(arm, dtype=dt).specialize()
+n = 1 << 20
+Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=556, dtype=dt,
+                           device=dev)
+asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+g = torch.Generator().manual_seed(90)
+SQ = torch.zeros((4, n), dtype=torch.float64)
+SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
+SQ[1] = 1.2
+SQ = SQ.to(dt).to(dev).contiguous()
+blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 15
+run = lambda: cp.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ)  # noqa: E731
+for _ in range(5):
+    r = run()
+torch.cuda.synchronize()
+ts = []
+for _ in range(blocks):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        r = run()
+    e1.record()
+    torch.cuda.synchronize()
+    ts.append(e0.elapsed_time(e1) / 20 * 1e3)
+chk = (float(r[0].double().abs().sum()), float(r[1].double().abs().sum()), float(r[2].double().sum()))
+print(f"scene median {statistics.median(ts):6.1f}us min {min(ts):6.1f}us chk {chk[0]:.9e} {chk[1]:.9e} {chk[2]:.9e}",
+      flush=True)
