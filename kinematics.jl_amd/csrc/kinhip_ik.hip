@@ -102,11 +102,14 @@ bool ik_wants_two_phase(const IkArgs& a, int64_t n, int64_t cap) {
 // 23% of the targets are still unsolved after 10 iterations (46% after 8, 4% after 16; oracle
 // histogram), so phase 2 keeps about one wave per SIMD; measured 0.081 ms vs 0.089 (no hand-over),
 // 0.092 (cut 8), 0.084 (cut 12) fp32 and 0.165 / 0.179 / 0.236 / 0.170 ms fp64
-// (profiles/r03_ik_handover.txt).  KINHIP_IK_P1_CUT=<iterations> overrides (A/B build; 0 disables).
+// (profiles/r03_ik_handover.txt).  With error-scaled damping (damp_err > 0) attempt 0 converges
+// sooner (93% within 10 iterations), and half an attempt is the faster cut: config 4 damped 0.079 ms
+// at cut 8 vs 0.088 at 10 (fixed lambda: 0.141 vs 0.082; profiles/r04_ik_p1_cut_ab.txt).
+// KINHIP_IK_P1_CUT=<iterations> overrides (A/B build; 0 disables).
 // 0 when the hand-over is not allowed or not shorter than L.
-static int ik_p1_cut(int L, bool allowed) {
+static int ik_p1_cut(int L, bool allowed, bool damped) {
     static const int env = ab_env_int("KINHIP_IK_P1_CUT", -1);
-    const int cut = env >= 0 ? env : (5 * L) / 8;
+    const int cut = env >= 0 ? env : damped ? L / 2 : (5 * L) / 8;
     return allowed && cut > 0 && cut < L ? cut : 0;
 }
 
@@ -199,7 +202,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             // of every handed-over target that attempt 0 still solves (1M targets: 0.55 -> 0.59 ms).
             // Not for in-place calls of based plans (the hand-over would overwrite the start pose that
             // attempts 1, 2, ... begin from).
-            const int cut = (c + 63) / 64 <= resident_waves ? ik_p1_cut(L, P.flags & PF_BASE ? (q0 != nullptr) : true) : 0;
+            const int cut = (c + 63) / 64 <= resident_waves ? ik_p1_cut(L, P.flags & PF_BASE ? (q0 != nullptr) : true, a.damp_err != 0.0) : 0;
             a1.p1_cut = cut;
             // phase 1 shares out targets like the one-phase schedule (one per lane while the batch
             // fills the chip in at most two rounds of waves, else wave-local queues) -- but a queue
