@@ -371,8 +371,72 @@ def _scene_and_coll_ik_legs(ctx, stream, n, steps, spec=1):
                               reps, warmup=1)
     out["f3_collision_ik"]["ms_stage2"] = dev2 / reps * 1e3
     out["f3_collision_ik"]["ms_stage1"] = out["f3_collision_ik"]["ms_per_batch"] - dev2 / reps * 1e3
+    # the same bistage solve against UnionSDF(fridge) attached to its mechanism, the door angle per target
+    # (kin_ik_coll_batch_scene; test/test_inverse_kinematics.jl:52-86, fridge_demo.jl's door)
+    SQ2 = torch.zeros((4, nt), dtype=torch.float64)
+    SQ2[0] = torch.rand(nt, generator=g, dtype=torch.float64) * 0.9 + 1.5
+    SQ2[1] = 1.2
+    SQ2 = SQ2.to(dt).to(ctx.device).contiguous()
+    out["f3_collision_ik_scene_door"] = _bistage_leg(ctx, stream, cplan, asdf, tg, Q0, nt, reps, scene_q=SQ2,
+                                                     spec=spec)
+    out["f3_pr2_collision_ik"] = _pr2_leg(ctx, stream, asdf, nt, reps, spec)
     for n_p in (4096, 65536):
         out[f"f3_collision_ik_pillar_{n_p}"] = _pillar_leg(ctx, stream, m, arm, sscc, sdf, n_p, spec)
+    return out
+
+
+def _bistage_leg(ctx, stream, cplan, sdf, tg, Q0, nt, reps, scene_q=None, spec=1):
+    """One CollisionIKPlan.solve per batch (stage 1 kin_ik_dls_batch_from + stage 2), timed, and stage 2 alone
+    from stage 1's answers."""
+    kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2, index_base=ctx.rank * nt)
+    wall, dev_s, (Qs, it, err) = _timed_calls(
+        ctx, stream, lambda: cplan.solve(sdf, tg, Q0, stream=stream, scene_q=scene_q, **kw), reps, warmup=1)
+    conv = it <= 128
+    Q1 = Q0.clone()
+    cplan.ik_dls(tg, Q1, Q0=Q0, **kw)
+    Q2 = torch.empty_like(Q0)
+    _, dev2, _ = _timed_calls(ctx, stream, lambda: cplan.ik_coll(sdf, tg, Q2, Q0=Q1, margin=0.02, stream=stream,
+                                                                 scene_q=scene_q, **kw), reps, warmup=1)
+    return {"value": nt * ctx.world * reps / wall, "unit": "bistage IK solves/s", "targets_per_gpu": nt,
+            "ms_per_batch": dev_s / reps * 1e3, "ms_stage2": dev2 / reps * 1e3,
+            "converged": float(conv.float().mean()),
+            "min_sphere_distance_converged": float(err[2][conv].min()) if bool(conv.any()) else None,
+            "kernels": "specialised" if spec else "generic"}
+
+
+def _pr2_leg(ctx, stream, asdf, nt, reps, spec):
+    """The reference's own collision-aware IK shape (test/test_inverse_kinematics.jl:52-86, fridge_demo.jl):
+    PR2 (tests/golden/pr2_two_arms.urdf) with its planar base, joints = vcat(rarm, larm) -- 14 joints + base =
+    17 variables -- spheres on both arms' collision links, the l_gripper_tool_frame target inside the fridge
+    (Transform((0, 0, 1.2)) * pose_fridge, jittered), the door angle per target, from reset_manip_pose.  fp32."""
+    dt = torch.float32
+    m = kinhip.parse_urdf(os.path.join(ROOT, "tests", "golden", "pr2_two_arms.urdf"), with_base=True)
+    joints = [m.find_joint(n) for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS]
+    m.set_joint_angles([m.find_joint("torso_lift_joint")], [0.3, 0.0, 0.0, 0.0])
+    sscc = kinhip.SweptSphereCollisionChecker(m)
+    for name, c, r in kinhip.PR2_ARM_SPHERES:
+        sscc.add_coll_sphere(m.find_link(name), c, r)
+    cplan = kinhip.CollisionIKPlan(sscc, m.find_link("l_gripper_tool_frame"), joints, dtype=dt)
+    if spec:
+        _specialize(cplan)
+    r, l, _ = kinhip.PR2_MANIP_POSE
+    q0 = np.concatenate([np.deg2rad(np.array(r + l)), np.zeros(3)])
+    Q0 = torch.tensor(np.repeat(q0[:, None], nt, 1), dtype=dt, device=ctx.device).contiguous()
+    rng = np.random.default_rng(29 + ctx.rank)
+    tg = np.zeros((12, nt))
+    for k in range(nt):
+        yaw = rng.uniform(-0.2, 0.2)
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        R = np.array([[c, -s_, 0.0], [s_, c, 0.0], [0.0, 0.0, 1.0]])
+        tg[:, k] = np.concatenate([R.T.reshape(-1), [1.2 + rng.uniform(-0.06, 0.0), rng.uniform(-0.06, 0.06),
+                                                     1.2 + rng.uniform(-0.05, 0.05)]])
+    tg = torch.tensor(tg, dtype=dt, device=ctx.device).contiguous()
+    SQ = torch.zeros((4, nt), dtype=torch.float64)
+    SQ[0] = torch.tensor(rng.uniform(1.6, 2.4, nt))
+    SQ[1] = 1.2
+    SQ = SQ.to(dt).to(ctx.device).contiguous()
+    out = _bistage_leg(ctx, stream, cplan, asdf, tg, Q0, nt, reps, scene_q=SQ, spec=spec)
+    out["variables"] = cplan.n_qcols
     return out
 
 

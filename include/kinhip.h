@@ -52,7 +52,10 @@ extern "C" {
 #endif
 
 #define KINHIP_API __attribute__((visibility("default")))
-#define KINHIP_ABI_VERSION 1
+/* ABI version (kin_abi_version): 2 since kin_ik_params gained damp_err (round 4) -- a caller built against
+ * version 1 passes a shorter kin_ik_params, so bindings check this value at load (the Python mirror and
+ * the Julia shim refuse a mismatch) and the library's soname is libkinhip.so.2. */
+#define KINHIP_ABI_VERSION 2
 
 typedef enum {
     KIN_OK = 0,
@@ -200,7 +203,9 @@ enum {
     KIN_SPEC_IK = 2u,        /* kin_ik_dls_batch (with_rot 0/1, every lane count) */
     KIN_SPEC_NAKAMURA = 4u,  /* kin_point_ik_nakamura_batch */
     KIN_SPEC_COLL = 8u,      /* kin_coll_batch, kin_ineq_const_batch (spheres folded; boxes stay data) */
-    KIN_SPEC_IK_COLL = 16u   /* kin_ik_coll_batch (plans of kin_coll_ik_plan_create) */
+    KIN_SPEC_IK_COLL = 16u,  /* kin_ik_coll_batch (plans of kin_coll_ik_plan_create) */
+    KIN_SPEC_IK_COLL_SCENE = 32u  /* kin_ik_coll_batch_scene over unions of <= 2 moving scene groups (the
+                                     scene's frames and boxes stay launch data: one code object per plan) */
 };
 KINHIP_API int kin_plan_specialize(kin_plan* p, uint32_t kernels);
 /* The KIN_SPEC_* mask the plan currently runs specialised. */
@@ -276,7 +281,8 @@ typedef struct kin_ik_params {
     double damp_err;    /* error-scaled damping (Levenberg-Marquardt after Sugihara): each iteration solves with
                            lambda^2 + damp_err * (|dp|^2 + |rot|^2) in place of lambda^2 -- heavy damping far from
                            the target, lambda near it.  0: fixed lambda.  kin_ik_dls_batch(_from) only (the
-                           collision-aware IK requires 0).  Config 4's bench runs 0.01 (tools/ik_damp_explore.py) */
+                           collision-aware IK requires 0).  Config 4's headline leg runs 0 (fixed lambda); the
+                           bench's config4_ik_dls_damped leg runs 0.01 with max_step 1 (tools/ik_damp_explore.py) */
 } kin_ik_params;
 KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                 void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde,
@@ -290,6 +296,17 @@ KINHIP_API int kin_ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, con
 KINHIP_API int kin_ik_dls_batch_from(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                      const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* err,
                                      int64_t lde, void* stream);
+
+/* kin_ik_dls_batch_from that also records the residual of every iterate: trace [2 (max_iters + 1)][ldtr]
+ * (dtype) gets |dp| (row 2k) and |rot err| (row 2k + 1) of iterate k = 0, 1, ... as the solver reaches it
+ * (rows of iterations a target does not reach are left as they are).  One lane per target (lanes is
+ * ignored, attempts in sequence).  This is what the reference's ftol_abs stopping rule needs (NLopt stops
+ * when one step changes the objective by less than ftol, src/inverse_kinematics.jl:23-30): one launch of
+ * max_iters steps gives every iterate's objective, a second of k steps the stopping iterate -- O(max_iters)
+ * steps (kinhip.inverse_kinematics_). */
+KINHIP_API int kin_ik_dls_batch_trace(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
+                                      const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* trace,
+                                      int64_t ldtr, void* stream);
 
 /* point_inverse_kinematics_nakamura (src/algorithm.jl:116-131), batched:
  * 50 SR-inverse iterations, `.+ sr_weight` broadcast quirk reproduced.
@@ -329,8 +346,9 @@ typedef struct kin_coll_desc {
     const double* centers;           /* ... plus this offset in the link frame ([n][3], NULL = 0) */
     const double* radii;             /* [n] */
 } kin_coll_desc;
-/* Every sphere must hang (through fixed / non-batched joints) off the chain of
- * batch joints of one arm (KIN_E_UNSUPPORTED otherwise). */
+/* Spheres may hang off several moving chains (e.g. both arms, or arm + head): the plan groups them by
+ * chain, stages one program per group and launches them in turn (min_dist accumulates); gradient
+ * columns of joints off a sphere's chain are 0.  Limits: kin_limits (KIN_E_UNSUPPORTED beyond). */
 KINHIP_API int kin_coll_plan_create(const kin_model* m, const kin_coll_desc* desc, kin_plan** out);
 /* compute_coll_dists(_and_grads)! for N configurations:
  *   dists    [n_spheres][ldd]       sdf(centre) - radius (or NULL)
@@ -357,8 +375,9 @@ KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double trun
 
 /* kin_coll_batch against boxes attached to a scene (kin_sdf_create_attached): scene_q [n_scene_cols][lds]
  * holds the scene joint values (+ base x, y, theta) of every sample -- one launch sweeps e.g. many door
- * angles -- or, with lds = 0, one set of values for the whole launch.  Plain SoA only; the generic
- * kernel runs (no plan specialisation for attached boxes). */
+ * angles -- or, with lds = 0, one set of values for the whole launch.  Plain SoA only.  Plans specialised
+ * with KIN_SPEC_COLL run kernels with the arm chain and spheres as constants (the scene's groups, steps
+ * and boxes stay launch data) for unions of up to 4 moving groups; the generic kernel otherwise. */
 KINHIP_API int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q,
                                     int64_t ldq, const void* scene_q, int64_t lds, int64_t n, void* dists,
                                     int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream);
@@ -373,7 +392,7 @@ KINHIP_API int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, doubl
  * may hang off any chain of the tree (both arms of a two-arm robot, torso / head links: the reference's
  * fridge_demo.jl scene); the solver's variables are the q joints that move the target link or a sphere
  * (+ the planar base), the other q columns are passed through.  Limits (KIN_E_UNSUPPORTED beyond):
- * q columns + 3 base columns <= 12, <= 32 moving joints on the needed tree, <= 64 spheres, at most 2 branch
+ * q columns + 3 base columns <= 24 (PR2's two arms + base: 17), <= 32 moving joints on the needed tree, <= 64 spheres, at most 2 branch
  * frames live at once.  Zero spheres is the plain pose problem (the reference's own PR2 test builds its
  * checker with none, test/test_inverse_kinematics.jl:63). */
 KINHIP_API int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* desc, int32_t link_id, kin_plan** out);
@@ -395,7 +414,8 @@ typedef struct kin_ik_coll_params {
  * lane groups for batches of at most 65,536 targets, its spheres shared out over 16 lanes per group
  * while the batch has at most ~4,096 targets), 1 = one lane per target (attempts in sequence),
  * 2 / 4 / 8 = attempts side by side on one lane each, 16 = spheres over 16 lanes, 64 = both (16 x 4);
- * identical results for every setting (the generic kernel runs one lane whatever lanes says).
+ * identical results for every setting (the generic kernel runs 4 attempt groups for lanes 2 / 4 / 8 on
+ * trees of <= 12 variables, one lane otherwise).
  * Converged (iters <= max_iters, else max_iters + 1) when |dp| < tol_pos, |rot| < tol_rot and every
  * sphere has d >= margin - feas; a target no attempt solves gets the attempt whose end state has the
  * lowest |dp|^2 + |rot|^2 + weight^2 max(0, margin - min d)^2 (NLopt returns its best point likewise).
@@ -408,7 +428,9 @@ KINHIP_API int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const ki
  * of fridge_demo.jl / test/test_inverse_kinematics.jl:52-86): scene_q [n_scene_cols][lds] holds the scene
  * joint values (+ base x, y, theta) of each target -- one launch solves e.g. a reach into the fridge at a
  * different door angle per target -- or, with lds = 0, one set for the whole launch.  The scene stays
- * fixed during a target's solve.  Runs the generic kernel (one lane per target). */
+ * fixed during a target's solve.  Lanes as kin_ik_coll_batch: plans specialised with
+ * KIN_SPEC_IK_COLL_SCENE run the S x G-lane kernels for unions of up to 2 moving groups (the fridge and
+ * its door), bit-identical to the generic kernel; wider scenes run the generic kernel. */
 KINHIP_API int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
                                        const kin_ik_coll_params* cprm, const void* target, int64_t ldt,
                                        const void* scene_q, int64_t lds, const void* q0, void* q, int64_t ldq,

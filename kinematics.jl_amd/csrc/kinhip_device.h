@@ -61,15 +61,33 @@ struct Fr {
 // reduction by pi/2 with FMA-split constants, minimax kernels on [-pi/4, pi/4]
 // (Cephes sinf/cosf for fp32, fdlibm __kernel_sin/__kernel_cos for fp64), and
 // the library call kept only behind a rarely taken |x| bound.
+// The large-|x| path returns its results BY VALUE (in VGPRs): no pointer into the caller's private
+// segment crosses the call.  Round 4 traced a MEMORY_APERTURE_VIOLATION in the generic fp64 four-lane
+// collision IK to the previous form, sincos_slow(x, float* s, float* c), whose out-parameters were flat
+// pointers to the caller's stack slots inside a kernel with SGPRs spilled to VGPR lanes
+// (profiles/r04_ikc_fault.txt); the callee's own sincos outputs are locals, promoted to registers.
+// tools/isa_check.py asserts over every product kernel that no flat access reaches private memory.
+template <typename T>
+struct SinCosV {
+    T s, c;
+};
 #ifndef KINHIP_NOCALL_TRIG
 #define KINHIP_NOCALL_TRIG 0  // 1 (A/B fault probe only): no out-of-line call; |x| beyond the bound -> NaN
 #endif
 #if KINHIP_NOCALL_TRIG
-__device__ __forceinline__ void sincos_slow(float x, float* s, float* c) { *s = *c = __builtin_nanf(""); }
-__device__ __forceinline__ void sincos_slow(double x, double* s, double* c) { *s = *c = __builtin_nan(""); }
+__device__ __forceinline__ SinCosV<float> sincos_slow(float) { return {__builtin_nanf(""), __builtin_nanf("")}; }
+__device__ __forceinline__ SinCosV<double> sincos_slow(double) { return {__builtin_nan(""), __builtin_nan("")}; }
 #else
-__device__ __noinline__ void sincos_slow(float x, float* s, float* c) { sincosf(x, s, c); }
-__device__ __noinline__ void sincos_slow(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __noinline__ SinCosV<float> sincos_slow(float x) {
+    float s, c;
+    sincosf(x, &s, &c);
+    return {s, c};
+}
+__device__ __noinline__ SinCosV<double> sincos_slow(double x) {
+    double s, c;
+    sincos(x, &s, &c);
+    return {s, c};
+}
 #endif
 
 __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
@@ -78,7 +96,9 @@ __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
             *s = *c = x - x;
             return;
         }
-        sincos_slow(x, s, c);
+        const SinCosV<float> r = sincos_slow(x);
+        *s = r.s;
+        *c = r.c;
         return;
     }
     const float j = rintf(x * 0.636619772367581343f);
@@ -100,7 +120,9 @@ __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
             *s = *c = x - x;
             return;
         }
-        sincos_slow(x, s, c);
+        const SinCosV<double> r = sincos_slow(x);
+        *s = r.s;
+        *c = r.c;
         return;
     }
     const double j = rint(x * 0.63661977236758134308);
@@ -267,6 +289,21 @@ template <typename T>
 __device__ __forceinline__ T mulz(T a, T F) {
     if (__builtin_constant_p(F) && F == T(0)) return T(0);
     return a * F;
+}
+
+// acc - a * b with the term dropped when a or b is a compile-time zero, and a * b = 0 when a is one: the
+// structural zeros of a specialised kernel's normal equations (variables that share no row, e.g. the two
+// arms of a two-arm robot) then cost no instruction in its factorisation.  Equal to fma(-a, b, acc) /
+// a * b for finite operands (up to the sign of a zero), so specialised and generic kernels agree.
+template <typename T>
+__device__ __forceinline__ T fnz(T a, T b, T acc) {
+    if ((__builtin_constant_p(a) && a == T(0)) || (__builtin_constant_p(b) && b == T(0))) return acc;
+    return fma(-a, b, acc);
+}
+template <typename T>
+__device__ __forceinline__ T mul0(T a, T b) {
+    if (__builtin_constant_p(a) && a == T(0)) return T(0);
+    return a * b;
 }
 
 // f <- f * F   (F: row-major 3x4 in uniform memory)

@@ -19,6 +19,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <sstream>
 #include <string>
 #include <type_traits>
@@ -225,6 +226,7 @@ struct kin_plan {
     mutable int ik_captured = 0;  // sets kIkEagerSets .. kIkEagerSets + ik_captured - 1 belong to graphs
     mutable hipEvent_t ik_ev[kIkEagerSets] = {};      // recorded after a set's last call (null: unused)
     mutable void* ik_stream[kIkEagerSets] = {};       // stream of that call
+    mutable std::thread::id ik_thread[kIkEagerSets];  // host thread of that call (per-thread stream handles)
     mutable bool ik_busy[kIkEagerSets] = {};          // a host thread is launching into the set
     mutable uint32_t ik_one_phase_fallbacks = 0;      // calls that found every set in flight (tests)
     // collision-aware IK program (kin_coll_ik_plan_create, k_ik_tree): the needed tree, host copies
@@ -1096,7 +1098,7 @@ int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
     if (const int rc = check_device(p->device, "kin_plan_specialize", "the plan")) return rc;
     uint32_t applies = 0;
     if (p->is_coll_ik) {
-        applies = KIN_SPEC_IK | KIN_SPEC_IK_COLL;
+        applies = KIN_SPEC_IK | KIN_SPEC_IK_COLL | KIN_SPEC_IK_COLL_SCENE;
     } else if (p->is_coll) {
         applies = KIN_SPEC_COLL;
     } else {
@@ -1944,7 +1946,8 @@ int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, con
 }
 
 static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, const void* q0,
-                        void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
+                        void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream,
+                        void* trace = nullptr, int64_t ldtr = 0) {
     if (!p || !prm) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: null argument");
     if (!p->ik_ok) return set_error(KIN_E_INVALID, "kin_ik_dls_batch: plan not usable for IK: " + p->ik_why);
     if (n < 0) return set_error(KIN_E_INVALID, "n < 0");
@@ -1962,6 +1965,12 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         return set_error(KIN_E_INVALID, "kin_ik_params.damp_err must be finite and >= 0");
     IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
              prm->restarts, prm->seed, prm->lanes, prm->index_base, prm->damp_err};
+    if (trace) {  // kin_ik_dls_batch_trace: one lane per target, attempts in sequence (rows by iteration)
+        if (ldtr < n) return set_error(KIN_E_INVALID, "kin_ik_dls_batch_trace: ldtr < n");
+        a.lanes = 1;
+        a.trace = trace;
+        a.trace_ld = ldtr;
+    }
     // the specialised IK kernels address rows with 32-bit offsets (ldn_soa): every lane offset of a
     // launch chunk plus rows * ld must stay below 2^31 bytes, else the generic kernel runs
     const int64_t esz = p->dtype == KIN_F32 ? 4 : 8;
@@ -2001,9 +2010,17 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                 }
             }
             if (!capturing) {
-                // the set this stream used last, else a finished one, else none (one phase)
+                // the set this stream used last, else a finished one, else none (one phase).  One handle
+                // names one stream for every host thread except hipStreamPerThread, which is each calling
+                // thread's own default stream: that handle matches only from the same thread.
+                // (The null stream is the device's legacy default stream, shared by every thread: this
+                // library is not built for per-thread default streams.)
+                const bool per_thread = (hipStream_t)stream == hipStreamPerThread;
+                const std::thread::id self = std::this_thread::get_id();
                 for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
-                    if (!p->ik_busy[k] && p->ik_ev[k] && p->ik_stream[k] == stream) set = k;
+                    if (!p->ik_busy[k] && p->ik_ev[k] && p->ik_stream[k] == stream &&
+                        (!per_thread || p->ik_thread[k] == self))
+                        set = k;
                 for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
                     if (!p->ik_busy[k] && (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess)) set = k;
                 if (set >= 0) {
@@ -2039,12 +2056,10 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                                   (hipStream_t)stream);
     if (eager_set >= 0) {  // the set is free again once this call has run on its stream
         std::lock_guard<std::mutex> lk(p->ik_mu);
-        if (hipEventRecord(p->ik_ev[eager_set], (hipStream_t)stream) == hipSuccess) {
-            p->ik_stream[eager_set] = stream;
-        } else {  // (cannot tell when it finishes: a fresh event, queried as finished, would lie)
-            (void)hipStreamSynchronize((hipStream_t)stream);
-            p->ik_stream[eager_set] = stream;
-        }
+        if (hipEventRecord(p->ik_ev[eager_set], (hipStream_t)stream) != hipSuccess)
+            (void)hipStreamSynchronize((hipStream_t)stream);  // (cannot tell when it finishes otherwise)
+        p->ik_stream[eager_set] = stream;
+        p->ik_thread[eager_set] = std::this_thread::get_id();
         p->ik_busy[eager_set] = false;
     }
     if (e != hipSuccess)
@@ -2065,6 +2080,13 @@ int kin_ik_dls_batch_from(const kin_plan* p, const kin_ik_params* prm, const voi
                           void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream) {
     if (!q0) return set_error(KIN_E_INVALID, "kin_ik_dls_batch_from: null q0");
     return ik_dls_batch(p, prm, target, ldt, q0 == q ? nullptr : q0, q, ldq, n, iters, err, lde, stream);
+}
+
+int kin_ik_dls_batch_trace(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
+                           const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* trace, int64_t ldtr,
+                           void* stream) {
+    if (!q0 || !trace) return set_error(KIN_E_INVALID, "kin_ik_dls_batch_trace: null q0 / trace");
+    return ik_dls_batch(p, prm, target, ldt, q0 == q ? nullptr : q0, q, ldq, n, iters, nullptr, 0, stream, trace, ldtr);
 }
 
 int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt, void* q, int64_t ldq, int64_t n,

@@ -1,7 +1,6 @@
 // kinhip_ik.hip -- k_ik_dls (batched DLS IK with restarts) and k_nakamura.
 // (gfx950 only; shared helpers in kinhip_device.h)
 #include "kinhip_ik_dev.h"
-#include "kinhip_ikt_dev.h"
 
 namespace kinhip {
 namespace {
@@ -25,20 +24,6 @@ __global__ __launch_bounds__(256) void k_nakamura(const KProg<T> P, const KStep<
                                                   const T* __restrict__ pts, int64_t ldpt, T* __restrict__ q,
                                                   int64_t ldq, int64_t n) {
     nakamura_body<T, MAXA>(P, S, pts, ldpt, q, ldq, n);
-}
-
-// generic collision-aware IK: one lane per target (attempts in sequence), the program from memory;
-// MAXG > 0: boxes attached to a scene, scene joint values per target
-template <typename T, int MAXV, int ROWS, int MAXG>
-__global__ __launch_bounds__(64) void k_ik_tree(const KIkcProg<T> P, const KIkcStep<T>* __restrict__ S,
-                                                const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
-                                                const CollArgs ca, const IkcArgsT<T> cz, const IkArgsT<T> a,
-                                                const SceneArgs<T> sa, const T* __restrict__ tgt, int64_t ldt,
-                                                T* __restrict__ q, int64_t ldq, int64_t n, int32_t* __restrict__ iters,
-                                                T* __restrict__ err, int64_t lde) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    ikt_body<T, MAXV, ROWS, 1, 1, 1, MAXG>(P, S, sph, boxes, ca, cz, a, sa, tgt, ldt, q, ldq, n, iters, err, lde,
-                                                 smem);
 }
 
 }  // namespace
@@ -70,11 +55,6 @@ static int ik_cus() {
 static int64_t ik_resident_waves() {
     static const int res_env = ab_env_int("KINHIP_IK_RESIDENT", 0);
     return (int64_t)ik_cus() * (res_env > 0 ? res_env : 8);
-}
-
-static void ik_attempts(const IkArgs& a, int* L, int* natt) {
-    *L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
-    *natt = (*L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / *L : 1;
 }
 
 // Two-phase schedule (KINHIP_IK_TWO_PHASE=<0|1> in the A/B build, default automatic): a chunk of
@@ -126,6 +106,8 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
                   0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
     at.damp_err = T(a.damp_err);
+    at.trace = (T*)a.trace;
+    at.trace_ld = a.trace_ld;
     const int G = ik_group(n, natt, a.lanes);
     const int cus = ik_cus();
     const int64_t resident_waves = ik_resident_waves();
@@ -141,19 +123,21 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     // KINHIP_IK_TP_QUEUE=<0|1> (A/B): phase 1 of a large batch on wave-local queues; default:
     // automatic (only where the queue's resident waves do not lower the kernel's occupancy)
     static const int tpq_env = ab_env_int("KINHIP_IK_TP_QUEUE", -1);
-    auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw) -> hipError_t {
-        const dim3 grid((unsigned)((nw * 64 + 255) / 256)), block(256);
+    auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw,
+                   int bs = 256) -> hipError_t {
+        const dim3 grid((unsigned)((nw * 64 + bs - 1) / bs)), block(bs);
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
+        if (at.trace) ar.trace = at.trace + s0;
         const hipFunction_t jk =
             jf ? jf->ik[a.with_rot ? 1 : 0][GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3] : nullptr;
         if (jk) {
             int64_t cc = c, pw = per_wave;
             void* args[] = {(void*)&ar, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
                             (void*)&ic, (void*)&ec, (void*)&lde, (void*)&pw};
-            return hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1, 0, st, args, nullptr);
+            return hipModuleLaunchKernel(jk, grid.x, 1, 1, (unsigned)bs, 1, 1, 0, st, args, nullptr);
         }
 #define KIN_IK_G(MA, R, GX) \
         hipLaunchKernelGGL((k_ik_dls<T, MA, R, GX>), grid, block, 0, st, P, steps, ar, tc, ldt, qc, ldq, c, ic, ec, lde, per_wave)
@@ -227,14 +211,32 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             a2.p1_cut = cut;
             a2.fail_aux = scr.fail_aux;
             a2.idx = scr.fail_list;
-            static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 1);  // (A/B: 0 = block-major waves)
-            a2.p2_spread = spread_env != 0 ? 1 : 0;
-            a2.fail_ctl = scr.fail_ctl;
-            a2.fail_mask = (uint32_t)(scr.ring_cap - 1);
             const int na2 = natt - a2.att0;
             const int G2 = na2 <= 1 ? 1 : na2 <= 2 ? 2 : na2 <= 4 ? 4 : 8;
             const int64_t ng2 = 64 / G2;
-            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2)) != hipSuccess) {
+            // Phase 2's list fills only the first waves of its grid (one wave per SIMD or less).  Its waves
+            // are dealt slot-major over the workgroups the chip holds at once (IkArgsT::p2_spread = the
+            // phase-2 kernel's resident workgroups): the first wave of each, then the second, ... -- a
+            // short list spreads over every CU, and a list of fewer waves than the resident workgroups
+            // hold never reaches a workgroup that has to wait for a slot.  Round 4 dealt the list over the
+            // WHOLE grid (4,096 workgroups at config 4): the fp64 kernel, two resident workgroups per CU,
+            // then ran a 1,000-wave list in two rounds of one busy wave per workgroup (config 4 fp64
+            // 0.145 -> 0.365 ms, BENCH_r04; A/B profiles/r05_ik_p2_ab.txt).  Generic kernels: block-major.
+            // KINHIP_IK_P2_SPREAD=<0|1|2 (whole grid)>, KINHIP_IK_P2_BLOCK=<64|256> (A/B build).
+            static const int p2_block_env = ab_env_int("KINHIP_IK_P2_BLOCK", 256);
+            static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 1);
+            const int bs2 = p2_block_env == 64 ? 64 : 256;
+            a2.p2_spread = 0;
+            if (spread_env != 0 && bs2 == 256 && jf) {  // (the resident workgroups of the phase-2 kernel)
+                const hipFunction_t f2 = jf->ik[a.with_rot ? 1 : 0][G2 == 1 ? 0 : G2 == 2 ? 1 : G2 == 4 ? 2 : 3];
+                int nb = 0;
+                if (f2 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f2, 256, 0) == hipSuccess && nb > 0)
+                    a2.p2_spread = spread_env == 2 ? (int)(((c + ng2 - 1) / ng2 * 64 + 255) / 256)  // (A/B: whole grid)
+                                                   : nb * cus;
+            }
+            a2.fail_ctl = scr.fail_ctl;
+            a2.fail_mask = (uint32_t)(scr.ring_cap - 1);
+            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2, bs2)) != hipSuccess) {
                 // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;
                 // the targets phase 1 did not solve keep undefined outputs (kin_ik_dls_batch says so)
                 (void)hipMemsetAsync(scr.fail_ctl, 0, sizeof(uint32_t) * kIkCtlStride * kIkSubRings, st);
@@ -248,92 +250,6 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         const int64_t per_wave = (c + waves - 1) / waves;  // targets each wave works through
         const int64_t nw = (c + per_wave - 1) / per_wave;
         const hipError_t e = one(at, G, s0, c, per_wave, nw);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
-// Lanes of a k_ik_tree target (specialised kernels): G attempt groups run a target's restart attempts
-// side by side, S sphere lanes per group share out its spheres -- identical results for every (S, G).
-// Small batches fill the chip only this way (the bistage solve's few thousand targets are a fraction of
-// a wave per SIMD): G = 4 while there are restart attempts and up to 2^16 targets, S = 16 while the
-// whole batch stays within ~4 waves per SIMD (n * G * 16 <= 2^18 lanes), else S = 1.
-// kin_ik_params.lanes forces a form: 1 = one lane, 2 / 4 / 8 = 4 attempt groups of one lane, 16 = 16
-// sphere lanes x 1, 64 = 16 x 4; KINHIP_IKT_S / KINHIP_IKT_G override (A/B build).
-static int ikt_variant(int64_t n, int natt, int lanes) {
-    static const int s_env = ab_env_int("KINHIP_IKT_S", 0), g_env = ab_env_int("KINHIP_IKT_G", 0);
-    if (lanes == 1) return 0;
-    if (lanes == 2 || lanes == 4 || lanes == 8) return 1;
-    if (lanes == 16) return 2;
-    if (lanes == 64) return 3;
-    int G = natt >= 2 && n <= (int64_t(1) << 16) ? 4 : 1;
-    int S = n * G * 16 <= (int64_t(1) << 18) ? 16 : 1;
-    if (s_env) S = s_env;
-    if (g_env) G = g_env;
-    for (int v = 0; v < kIktVariants; ++v)
-        if (kIktS[v] == S && kIktG[v] == G) return v;
-    return 0;
-}
-
-template <typename T>
-hipError_t launch_ik_tree(const KIkcProg<T>& P, const KIkcStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
-                          const CollArgs& ca, const SceneLaunch* scene, const IkcArgs& c, const IkArgs& a,
-                          const T* target, int64_t ldt, const T* q0, T* q, int64_t ldq, int64_t n, int32_t* iters,
-                          T* err, int64_t lde, const JitFns* jf, hipStream_t st) {
-    int L, natt;
-    ik_attempts(a, &L, &natt);
-    IkArgsT<T> at{a.max_iters, T(a.lambda * a.lambda), T(a.tol_pos), T(a.tol_rot), T(a.max_step), L, natt, a.seed,
-                  0, 0, 0, nullptr, nullptr, nullptr, 0u, nullptr, a.with_rot == 2 ? 1 : 0};
-    const IkcArgsT<T> cz{T(c.margin), T(c.band), T(c.weight), T(c.feas)};
-    const size_t lds = ca.n_boxes <= kCollLdsBoxes ? (size_t)ca.n_boxes * sizeof(KBox<T>) : 0;
-    const int rows6 = a.with_rot ? 1 : 0;
-    // the specialised kernels take a static union; a scene's union runs the generic kernel
-    const int vi = (jf && !scene) ? ikt_variant(n, natt, a.lanes) : 0;
-    const hipFunction_t jk = (jf && !scene) ? jf->ikt[rows6][vi] : nullptr;
-    const int lanes = jk ? kIktS[vi] * kIktG[vi] : 1;
-    SceneArgs<T> sa{};
-    if (scene) {
-        sa.groups = (const KSceneGroup*)scene->groups;
-        sa.steps = (const KSceneStep<T>*)scene->steps;
-        sa.q = (const T*)scene->q;
-        sa.ld = scene->ld;
-        sa.ng = scene->ng;
-        sa.base_col = scene->base_col;
-        sa.uniform = scene->uniform;
-    }
-    for (int64_t s0 = 0; s0 < n; s0 += kIkChunk) {
-        const int64_t cn = std::min(kIkChunk, n - s0);
-        at.ibase = a.index_base + s0;
-        at.q0 = q0 ? q0 + s0 : nullptr;
-        const T* tc = target + s0;
-        T* qc = q + s0;
-        int32_t* ic = iters ? iters + s0 : iters;
-        T* ec = err ? err + s0 : err;
-        SceneArgs<T> sac = sa;
-        if (scene && !sa.uniform) sac.q = sa.q + s0;
-        const unsigned grid = (unsigned)((cn * lanes + 63) / 64);
-        if (jk) {
-            int64_t cc = cn;
-            CollArgs cac = ca;
-            IkcArgsT<T> czc = cz;
-            void* args[] = {(void*)&boxes, (void*)&cac, (void*)&czc, (void*)&at, (void*)&tc, (void*)&ldt,
-                            (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&ic, (void*)&ec, (void*)&lde};
-            const hipError_t e = hipModuleLaunchKernel(jk, grid, 1, 1, 64, 1, 1, (unsigned)lds, st, args, nullptr);
-            if (e != hipSuccess) return e;
-            continue;
-        }
-#define KIN_IKT(MV, R, MG) \
-        hipLaunchKernelGGL((k_ik_tree<T, MV, R, MG>), dim3(grid), dim3(64), lds, st, P, steps, sph, boxes, ca, cz, at, sac, tc, ldt, qc, ldq, cn, ic, ec, lde)
-        // (variables bound 8 or 12: the normal equations and joint records live in registers)
-        if (scene) {
-            if (a.with_rot) KIN_IKT(kIkcMaxVars, 6, kMaxSceneGroups); else KIN_IKT(kIkcMaxVars, 3, kMaxSceneGroups);
-        } else if (P.nv <= 8) {
-            if (a.with_rot) KIN_IKT(8, 6, 0); else KIN_IKT(8, 3, 0);
-        } else {
-            if (a.with_rot) KIN_IKT(kIkcMaxVars, 6, 0); else KIN_IKT(kIkcMaxVars, 3, 0);
-        }
-#undef KIN_IKT
-        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -368,11 +284,7 @@ hipError_t launch_nakamura(const KProg<T>& P, const KStep<T>* steps, const Launc
                                          const T*, int64_t, const T*, T*, int64_t, int64_t, int32_t*, T*, int64_t, \
                                          const JitFns*, const IkScratch&, hipStream_t);                                         \
     template hipError_t launch_nakamura<T>(const KProg<T>&, const KStep<T>*, const LaunchGeom&, const T*,    \
-                                           int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);          \
-    template hipError_t launch_ik_tree<T>(const KIkcProg<T>&, const KIkcStep<T>*, const KSphere<T>*,          \
-                                          const KBox<T>*, const CollArgs&, const SceneLaunch*, const IkcArgs&,   \
-                                          const IkArgs&, const T*, int64_t, const T*, T*, int64_t, int64_t,      \
-                                          int32_t*, T*, int64_t, const JitFns*, hipStream_t);
+                                           int64_t, T*, int64_t, int64_t, const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

@@ -23,9 +23,20 @@ namespace {
 // the J rounding alone by 1e-6 (tools/ik_fp32_solve_error.py).  0: the fp32 solve (A/B build).  2: the
 // fp32 factorisation and solve plus one step of iterative refinement whose residual
 // e - (J W J^T + lambda'^2 I) y is formed in fp64 from J itself (J^T y, then J (W J^T y)), never from
-// the rounded J J^T: the fp32 factor contracts the error by ~eps kappa ~ 1e-3 per step.
+// the rounded J J^T: the fp32 factor contracts the error by ~eps kappa ~ 1e-3 per step.  3: the fp64
+// solve for the first KINHIP_IK_F64_ITERS iterations of attempt 0 only -- the attempt that starts from
+// the caller's q0, which for config 4 (and any caller starting from a zero / home pose) is a singular
+// arm (Fetch at q = 0: rank 4) -- and the fp32 solve everywhere else.  Along config-4 trajectories the
+// fp32 solve's step error (fp32 normal equations vs fp64, the same fp32 J) is <= 8.4e-4 at iteration 0,
+// 5.5e-4 at 1, 4.3e-4 at 2 and <= 1.8e-4 from iteration 3 on, 99.4% of the lanes <= 1e-5 there; restart
+// attempts start from random angles (tools/ik_cond_explore.py).  The choice is a function of the lane's
+// own attempt and iteration, so every lane layout / schedule still gives identical results, and phase 1
+// of the two-phase schedule (every lane at the same iteration) takes one path per wave.
 #ifndef KINHIP_IK_F64SOLVE
-#define KINHIP_IK_F64SOLVE 1
+#define KINHIP_IK_F64SOLVE 3
+#endif
+#ifndef KINHIP_IK_F64_ITERS
+#define KINHIP_IK_F64_ITERS 3
 #endif
 // Contraction only inside one expression (a * b + c): the specialised kernels (hiprtc) fold constants
 // into the instruction stream, and fusing across statements would then differ from the generic ones
@@ -202,9 +213,15 @@ struct IkArgsT {
     int32_t* fail_aux;
     // error-scaled damping (kin_ik_params.damp_err): the solve's lambda^2 + damp_err (|dp|^2 + |rot|^2)
     T damp_err;
-    // phase 2: list entries go to the first wave of every workgroup, then the second, ... (1), so that a
-    // short list spreads over all CUs instead of filling the first workgroups' CUs two waves per SIMD
+    // phase 2 (> 0): list entries go to the first wave of each of the first p2_spread workgroups (the
+    // workgroups the chip holds at once), then the second wave of each, ...: a short list spreads over all
+    // CUs instead of filling the first workgroups' CUs two waves per SIMD, and never reaches past the
+    // resident workgroups while it has fewer waves than they hold.  0: block-major waves.
     int32_t p2_spread;
+    // kin_ik_dls_batch_trace: |dp| and |rot| of every iterate (rows 2 it, 2 it + 1 of [2 (max_iters + 1)]
+    // [trace_ld]), or null
+    T* trace;
+    int64_t trace_ld;
 };
 
 // lambda^2 + mu (ep^2 + er^2) rounded operation by operation, as the oracle forms it (no contraction)
@@ -301,8 +318,12 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                                         int64_t chunk) {
     const int lane = (int)(threadIdx.x & 63u);
     const int slot = lane % G, grp = lane / G;
-    const int64_t wave = (a.idx && a.p2_spread) ? (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x
-                                                : ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (a.idx && a.p2_spread > 0) {  // rounds of p2_spread workgroups of 4 waves, wave slot-major in a round
+        const uint32_t R = (uint32_t)a.p2_spread, b = blockIdx.x, r0 = b / R * R;
+        const uint32_t rr = gridDim.x - r0 < R ? gridDim.x - r0 : R;
+        wave = (int64_t)r0 * 4 + (int64_t)(threadIdx.x >> 6) * rr + (b - r0);
+    }
     // two-phase control words (see IkArgsT): one lane per ring of the grid's first wave moves its start marks
     if (blockIdx.x == 0 && threadIdx.x < (unsigned)kIkSubRings && (a.phase1 || a.idx)) {
         uint32_t* c = a.fail_ctl + threadIdx.x * kIkCtlStride;
@@ -521,6 +542,10 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             e[3] = w[0]; e[4] = w[1]; e[5] = w[2];
             er = sqrt_fast(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
         }
+        if (a.trace) {  // (uniform) kin_ik_dls_batch_trace: this iterate's residual norms
+            st_soa(a.trace, 2 * (int64_t)it, a.trace_ld, off, ep);
+            st_soa(a.trace, 2 * (int64_t)it + 1, a.trace_ld, off, er);
+        }
         // the rare ends of an iteration behind one branch (bitwise, so the common path carries no
         // exec-mask bookkeeping): converged, out of iterations (only the last attempt gets there),
         // attempt over (phase 1 with a hand-over: the target goes to phase 2)
@@ -549,22 +574,6 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
 
         KIN_IK_STAMP(2);
-        // the damped solve's arithmetic type: fp64 (also in the fp32 kernel, KINHIP_IK_F64SOLVE)
-        using TS = typename ik_solve_type<sizeof(T) == 4 && KINHIP_IK_F64SOLVE != 1>::type;
-        constexpr bool refine = sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 2;
-        using YS = typename ik_solve_type<!refine && sizeof(TS) == 4>::type;  // type of the solution y
-        TS Jb[3][ROWS];
-        if (base) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-#pragma unroll
-                for (int r = 0; r < ROWS; ++r) Jb[k][r] = TS(0);
-            Jb[0][0] = TS(1);
-            Jb[1][1] = TS(1);
-            Jb[2][0] = -(TS)(Lf.t[1] - b[1]);
-            Jb[2][1] = (TS)(Lf.t[0] - b[0]);
-            if constexpr (ROWS == 6) Jb[2][5] = TS(1);
-        }
         // linear Jacobian rows z x (p - o) once per iteration (the solve and dq reuse them)
 #pragma unroll
         for (int s = 0; s < MAXA; ++s) {
@@ -593,7 +602,23 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         // (the re-solve ran in ~half of all lane-iterations, i.e. in nearly every wave-iteration).
         T dq[MAXA], db[3] = {T(0), T(0), T(0)};
         T mx = T(0);
-        {
+        // the damped solve in arithmetic type TS: fp64 (also in the fp32 kernel, KINHIP_IK_F64SOLVE)
+        auto damped_solve = [&](auto ts_tag) {
+            using TS = decltype(ts_tag);
+            constexpr bool refine = sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 2;
+            using YS = typename ik_solve_type<!refine && sizeof(TS) == 4>::type;  // type of the solution y
+            TS Jb[3][ROWS];
+            if (base) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+#pragma unroll
+                    for (int r = 0; r < ROWS; ++r) Jb[k][r] = TS(0);
+                Jb[0][0] = TS(1);
+                Jb[1][1] = TS(1);
+                Jb[2][0] = -(TS)(Lf.t[1] - b[1]);
+                Jb[2][1] = (TS)(Lf.t[0] - b[0]);
+                if constexpr (ROWS == 6) Jb[2][5] = TS(1);
+            }
             // A = J W J^T + lambda^2 I  (lower triangle)
             TS A[ROWS][ROWS];
             // (damp_err is uniform: a fixed-lambda call runs no extra instructions)
@@ -783,6 +808,13 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                     mx = fmax(mx, fabs(db[k]));
                 }
             }
+        };
+        if constexpr (sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3) {
+            // fp64 for the first iterations of attempt 0 (the caller's q0), fp32 elsewhere (see the macro)
+            if (att == 0 && it < KINHIP_IK_F64_ITERS) damped_solve(double());
+            else damped_solve(float());
+        } else {
+            damped_solve(typename ik_solve_type<sizeof(T) == 4 && KINHIP_IK_F64SOLVE != 1>::type());
         }
         KIN_IK_STAMP(5);
         const T sc = mx > a.max_step ? a.max_step / mx : T(1);

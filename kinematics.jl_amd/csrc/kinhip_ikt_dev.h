@@ -538,7 +538,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         for (int j = 0; j < MAXV; ++j) {
             T d = A[j][j];
 #pragma unroll
-            for (int k = 0; k < j; ++k) d = fma(-A[j][k], A[j][k], d);
+            for (int k = 0; k < j; ++k) d = fnz(A[j][k], A[j][k], d);
             T id;
             if constexpr (fast) {
                 id = rsqrt_fast(d);
@@ -552,15 +552,15 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             for (int r = j + 1; r < MAXV; ++r) {
                 T sm = A[r][j];
 #pragma unroll
-                for (int k = 0; k < j; ++k) sm = fma(-A[r][k], A[j][k], sm);
-                A[r][j] = sm * id;
+                for (int k = 0; k < j; ++k) sm = fnz(A[r][k], A[j][k], sm);
+                A[r][j] = mul0(sm, id);
             }
         }
 #pragma unroll
         for (int r = 0; r < MAXV; ++r) {
             T sm = y[r];
 #pragma unroll
-            for (int k = 0; k < r; ++k) sm = fma(-A[r][k], y[k], sm);
+            for (int k = 0; k < r; ++k) sm = fnz(A[r][k], y[k], sm);
             if constexpr (fast) y[r] = sm * ip[r];
             else y[r] = sm / A[r][r];
         }
@@ -568,7 +568,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         for (int r = MAXV - 1; r >= 0; --r) {
             T sm = y[r];
 #pragma unroll
-            for (int k = r + 1; k < MAXV; ++k) sm = fma(-A[k][r], y[k], sm);
+            for (int k = r + 1; k < MAXV; ++k) sm = fnz(A[k][r], y[k], sm);
             if constexpr (fast) y[r] = sm * ip[r];
             else y[r] = sm / A[r][r];
         }

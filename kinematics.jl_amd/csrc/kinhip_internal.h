@@ -58,6 +58,7 @@ struct JitFns {
     // collision-aware IK (k_ik_tree) [rows == 6][lanes: 0 = 1 x 1, 1 = 1 sphere lane x 4 attempt groups,
     // 2 = 16 sphere lanes x 1, 3 = 16 x 4] (kIktVariants)
     hipFunction_t ikt[2][4] = {};
+    hipFunction_t ikts[2][4] = {};  // the same over a union attached to a scene of at most 2 moving groups
 };
 // sphere lanes S and attempt groups G of the specialised k_ik_tree kernels, by JitFns::ikt index
 constexpr int kIktVariants = 4;
@@ -79,7 +80,15 @@ struct IkArgs {
     int32_t lanes;  // 0 auto
     int64_t index_base;  // global index of target 0 (restart draws)
     double damp_err;     // error-scaled damping (k_ik_dls only)
+    void* trace = nullptr;  // kin_ik_dls_batch_trace: [2 (max_iters + 1)][trace_ld] residual norms per iterate
+    int64_t trace_ld = 0;
 };
+
+// restart schedule of kin_ik_params: attempt length L (0: no restarts) and the attempts it reaches
+inline void ik_attempts(const IkArgs& a, int* L, int* natt) {
+    *L = a.restarts > 0 ? a.max_iters / (a.restarts + 1) : 0;
+    *natt = (*L > 0 && a.max_iters > 0) ? 1 + (a.max_iters - 1) / *L : 1;
+}
 
 // Device scratch of the two-phase IK schedule (launch_ik_dls): the list of targets attempt 0 did
 // not solve and its length, for batches of up to `cap` targets (null: single phase only)

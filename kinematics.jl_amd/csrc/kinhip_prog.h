@@ -137,7 +137,7 @@ constexpr int kMaxSceneGroups = 4;  // moving frames carrying boxes (per-lane fr
 // m.angles) are folded into F on the host in fp64 as joint_transform does (src/mechanism.jl:90-103);
 // frames are canonical (the joint axis on local z) as in KStep.  Spheres hang off a step's
 // post-motion frame (or the root frame); the target link's frame is frame(tgt_step) * Xt.
-constexpr int kIkcMaxVars = 12;   // q columns + 3 base columns (normal equations in registers)
+constexpr int kIkcMaxVars = 24;   // q columns + 3 base columns (normal equations in registers; PR2: 14 + 3)
 constexpr int kIkcMaxSteps = 32;  // moving joints on the needed tree
 constexpr int kIkcMaxSlots = 2;   // saved branch frames live at once
 constexpr int kIkcMaxSpheres = 64;

@@ -24,6 +24,12 @@ using Kinematics
 using AMDGPU
 
 const libkinhip = joinpath(@__DIR__, "..", "lib", "libkinhip.so")
+const KINHIP_ABI_VERSION = 2  # include/kinhip.h: the layout of KinIkParams below
+
+function __init__()
+    v = ccall((:kin_abi_version, libkinhip), Cint, ())
+    v == KINHIP_ABI_VERSION || error("$libkinhip: C-ABI version $v, KinematicsHIP needs $KINHIP_ABI_VERSION (rebuild)")
+end
 
 const KIN_F32 = Int32(0)
 const KIN_F64 = Int32(1)
@@ -446,13 +452,19 @@ end
 
 """Batched collision-aware IK, inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
 (src/inverse_kinematics.jl:1-21) for every row of `targets` (N, 12): stage 1 the collision-free DLS
-(kin_ik_dls_batch_from, seeds Q0), stage 2 kin_ik_coll_batch (the IneqConst(sscc, joints, sdf, 1, margin)
-sphere rows), both on one plan of kin_coll_ik_plan_create.  Returns (Q, iters, err (N, 3))."""
+(kin_ik_dls_batch_from, seeds Q0), stage 2 the IneqConst(sscc, joints, sdf, 1, margin) sphere rows, both on
+one plan of kin_coll_ik_plan_create.  A static `HIPSDF(UnionSDF)` runs kin_ik_coll_batch; an attached one
+(`HIPSDF(fridge, [door_joint])`, the reference's `UnionSDF(fridge)` of test/test_inverse_kinematics.jl:55
+and fridge_demo.jl) runs kin_ik_coll_batch_scene with `scene_q`: the scene columns per target, an
+(N, n_scene_cols) ROCMatrix (e.g. a door angle per target), or one ROCVector for the whole batch.
+Returns (Q, iters, err (N, 3))."""
 function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
                                         Q0::ROCMatrix{T}, sscc::Kinematics.SweptSphereCollisionChecker, sdf::HIPSDF;
                                         use_bistage=true, margin=0.02, band=0.0, weight=1.0, feas=1e-6,
                                         max_iters=64, lambda=1e-2, tol_pos=1e-3, tol_rot=1e-3, max_step=0.5,
-                                        rpy_objective=true, restarts=3, seed=0, index_base=0) where {T}
+                                        rpy_objective=true, restarts=3, seed=0, index_base=0,
+                                        scene_q=nothing) where {T}
+    sdf.attached && scene_q === nothing && throw(ArgumentError("an attached HIPSDF needs scene_q"))
     N = size(Q0, 1)
     ids = Int32[j.id for j in joints]
     sph = Int32[l.id for l in sscc.sphere_links]
@@ -484,6 +496,15 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
         copyto!(Q1, Q0)
     end
     cprm = KinIkCollParams(margin, band, weight, feas)
+    if sdf.attached
+        lds = scene_q isa ROCMatrix ? stride(scene_q, 2) : 0  # (N, cols) per target, or one vector
+        check(ccall((:kin_ik_coll_batch_scene, libkinhip), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Int64,
+                     Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),
+                    p, sdf.handle, prm, cprm, pointer(targets), stride(targets, 2), pointer(scene_q), lds,
+                    pointer(Q1), pointer(Q), stride(Q, 2), N, pointer(iters), pointer(err), N, stream_ptr()))
+        return Q, iters, err
+    end
     check(ccall((:kin_ik_coll_batch, libkinhip), Cint,
                 (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64,
                  Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),

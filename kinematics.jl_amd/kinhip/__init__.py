@@ -5,7 +5,10 @@ Python host mirror of the reference's API over the C-ABI library
 engine only; importing this package on a machine without the built library
 fails loudly.
 """
-from ._lib import KIN_SPEC_COLL, KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_IK_COLL, KIN_SPEC_NAKAMURA, KinError, LIB_PATH, lib  # noqa: F401
+from ._lib import (  # noqa: F401
+    KIN_SPEC_COLL, KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_IK_COLL, KIN_SPEC_IK_COLL_SCENE, KIN_SPEC_NAKAMURA, KinError, LIB_PATH,
+    lib,
+)
 from .mechanism import (  # noqa: F401
     BoxMetaData, Joint, Link, Mechanism, Plan, SphereMetaData, Transform, add_new_link, child_joints, child_link,
     child_links, find_joint, find_link, get_jacobian, get_jacobian_, get_jacobian_batch, get_joint_angles,
@@ -15,7 +18,8 @@ from .mechanism import (  # noqa: F401
 )
 from .synth import uniform_configs  # noqa: F401
 from .collision import (  # noqa: F401
-    FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, AttachedUnionSDF, BoxSDF, CollisionIKPlan, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
+    FETCH_ARM_SPHERES, FETCH_LINK_SPHERES, PR2_ARM_SPHERES, PR2_LARM_JOINTS, PR2_MANIP_POSE, PR2_RARM_JOINTS,
+    AttachedUnionSDF, BoxSDF, CollisionIKPlan, CollisionPlan, SweptSphereCollisionChecker, UnionSDF,
     add_coll_links, add_fetch_arm_spheres, compute_coll_dists, compute_coll_dists_, compute_coll_dists_and_grads,
     compute_coll_dists_and_grads_, compute_swept_sphere, fridge_sdf,
 )

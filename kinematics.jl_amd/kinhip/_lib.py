@@ -23,6 +23,8 @@ KIN_F32, KIN_F64 = 0, 1
 KIN_JOINT_FIXED, KIN_JOINT_REVOLUTE, KIN_JOINT_PRISMATIC = 0, 1, 2
 KIN_WITH_ROT, KIN_RPY_JAC, KIN_ZERO_FILL = 1, 2, 4
 KIN_SPEC_FK, KIN_SPEC_IK, KIN_SPEC_NAKAMURA, KIN_SPEC_COLL, KIN_SPEC_IK_COLL = 1, 2, 4, 8, 16
+KIN_SPEC_IK_COLL_SCENE = 32
+ABI_VERSION = 2  # KINHIP_ABI_VERSION of include/kinhip.h (kin_ik_params layout)
 
 # every entry point include/kinhip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -35,7 +37,7 @@ EXPORTS = [
     "kin_plan_create", "kin_plan_destroy", "kin_plan_shape", "kin_plan_run", "kin_plan_run_tiled",
     "kin_plan_specialize", "kin_plan_specialized", "kin_jit_selfcheck",
     "kin_get_transform_batch", "kin_get_jacobian_batch",
-    "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_point_ik_nakamura_batch",
+    "kin_ik_dls_batch", "kin_ik_dls_batch_from", "kin_ik_dls_batch_trace", "kin_point_ik_nakamura_batch",
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
     "kin_ineq_const_batch", "kin_pose_const_batch",
     "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
@@ -125,6 +127,7 @@ def lib():
         "kin_get_jacobian_batch": ([P, I32, I32, I32, P, U32, P, I64, I64, P, I64, P, I64, P], C.c_int),
         "kin_ik_dls_batch": ([P, P, P, I64, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_ik_dls_batch_from": ([P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
+        "kin_ik_dls_batch_trace": ([P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_point_ik_nakamura_batch": ([P, P, I64, P, I64, I64, P], C.c_int),
         "kin_sdf_create_boxes": ([I32, P, P, P], C.c_int),
         "kin_sdf_destroy": ([P], C.c_int),
@@ -144,6 +147,9 @@ def lib():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    if not os.environ.get("KINHIP_LIB") and L.kin_abi_version() != ABI_VERSION:
+        raise KinError(KIN_E_INVALID, f"{LIB_PATH}: C-ABI version {L.kin_abi_version()}, this binding needs "
+                                      f"{ABI_VERSION} (kin_ik_params layout); rebuild the library")
     _lib = L
     return L
 

@@ -253,8 +253,10 @@ class CollisionIKPlan(Plan):
         self.device_index = _current_device_index()
 
     def specialize(self, kernels: int = 0) -> "CollisionIKPlan":
-        """kin_plan_specialize (default: both stages' kernels, KIN_SPEC_IK | KIN_SPEC_IK_COLL)."""
-        K.check(K.lib().kin_plan_specialize(self._h, int(kernels) or (K.KIN_SPEC_IK | K.KIN_SPEC_IK_COLL)))
+        """kin_plan_specialize (default: both stages' kernels over static and attached unions,
+        KIN_SPEC_IK | KIN_SPEC_IK_COLL | KIN_SPEC_IK_COLL_SCENE)."""
+        K.check(K.lib().kin_plan_specialize(
+            self._h, int(kernels) or (K.KIN_SPEC_IK | K.KIN_SPEC_IK_COLL | K.KIN_SPEC_IK_COLL_SCENE)))
         return self
 
     def ik_coll(self, sdf, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
@@ -384,6 +386,22 @@ FETCH_ARM_SPHERES = [
     ("gripper_link", (-0.05, 0.0, 0.0), 0.05),
     ("gripper_link", (0.0, 0.0, 0.0), 0.045),
 ]
+
+
+# The same for the PR2 arms of tests/golden/pr2_two_arms.urdf: the links of rarm_collision_links /
+# larm_collision_links (src/models.jl:39-57), upper arm and forearm along +x, palm and fingers.
+PR2_ARM_SPHERES = [
+    (side + name, c, r) for side in ("r_", "l_") for name, c, r in (
+        ("upper_arm_link", (0.1, 0.0, 0.0), 0.1), ("upper_arm_link", (0.26, 0.0, 0.0), 0.085),
+        ("forearm_link", (0.1, 0.0, 0.0), 0.07), ("forearm_link", (0.22, 0.0, 0.0), 0.06),
+        ("gripper_palm_link", (0.06, 0.0, 0.0), 0.055),
+        ("gripper_r_finger_link", (0.04, 0.0, 0.0), 0.025), ("gripper_l_finger_link", (0.04, 0.0, 0.0), 0.025))
+]
+PR2_RARM_JOINTS = ["r_shoulder_pan_joint", "r_shoulder_lift_joint", "r_upper_arm_roll_joint", "r_elbow_flex_joint",
+                   "r_forearm_roll_joint", "r_wrist_flex_joint", "r_wrist_roll_joint"]  # src/models.jl:13-24
+PR2_LARM_JOINTS = [n.replace("r_", "l_", 1) for n in PR2_RARM_JOINTS]                  # src/models.jl:26-37
+# reset_manip_pose (src/models.jl:59-70): rarm, larm (degrees), torso
+PR2_MANIP_POSE = ([-75., 50., -110., -110., 20., -10., -10.], [75., 50., 110., -110., -20., -10., -10.], 0.3)
 
 
 # per-link table used by add_coll_links (the arm spheres above plus the torso column)

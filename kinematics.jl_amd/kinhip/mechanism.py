@@ -372,6 +372,25 @@ class Plan:
                                              N, iters.data_ptr(), err.data_ptr(), N, st))
         return Q, iters, err
 
+    def ik_dls_trace(self, targets: torch.Tensor, Q0: torch.Tensor, max_iters=64, lam=1e-2, tol_pos=1e-3,
+                     tol_rot=1e-3, max_step=0.5, with_rot=True, restarts=0, seed=0, index_base=0, stream=None,
+                     damp_err=0.0):
+        """``kin_ik_dls_batch_trace``: ik_dls from Q0 that also records |dp| and |rot| of every iterate ->
+        (Q, iters [N], trace [max_iters + 1, 2, N]); rows of iterations a target does not reach are NaN."""
+        N = self._check_q(Q0)
+        if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
+            raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
+        _same_device(targets, Q0, "targets")
+        Q = torch.empty_like(Q0)
+        iters = torch.empty(N, dtype=torch.int32, device=Q0.device)
+        trace = torch.full((int(max_iters) + 1, 2, N), float("nan"), dtype=self.dtype, device=Q0.device)
+        prm = K.IkParams(int(max_iters), float(lam), float(tol_pos), float(tol_rot), float(max_step), int(with_rot),
+                         int(restarts), int(seed), 1, int(index_base), float(damp_err))
+        st = (stream or torch.cuda.current_stream(Q0.device)).cuda_stream
+        K.check(K.lib().kin_ik_dls_batch_trace(self._h, C.byref(prm), targets.data_ptr(), N, Q0.data_ptr(),
+                                               Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), trace.data_ptr(), N, st))
+        return Q, iters, trace
+
     def point_ik_nakamura(self, points: torch.Tensor, Q: torch.Tensor, stream=None):
         N = self._check_q(Q)
         if points.shape != (3, N) or points.dtype != self.dtype or not points.is_contiguous():
@@ -725,8 +744,9 @@ def inverse_kinematics_(m: Mechanism, link: Link, joints, target_pose, sscc=None
     Without ``sscc`` / ``sdf`` (src/inverse_kinematics.jl:23-30): the DLS kernel on the reference's
     objective (f_objective: |[p* - p; rpy* - rpy]|^2, kin_ik_params.with_rot = 2), stopped by the
     reference's ``ftol_abs`` rule (NLopt stops when one step changes the objective by less than
-    ftol): the k-th iterate is one launch of k steps from the starting angles (the solver's active
-    set lives inside the kernel), so the rule is checked after every step.  Status ``:FTOL_REACHED`` when that rule
+    ftol), checked after every step on the objective of every iterate (kin_ik_dls_batch_trace: one
+    launch of max_iters steps), the stopping iterate k then one launch of k steps from the starting
+    angles.  Status ``:FTOL_REACHED`` when that rule
     stopped it, ``:MAXEVAL_REACHED`` after ``max_iters`` steps.
 
     With ``sscc`` and ``sdf`` (src/inverse_kinematics.jl:1-21): the collision-aware form.  Stage 1
@@ -757,29 +777,20 @@ def _dls_ik_ftol(m: Mechanism, link: Link, joints, target_pose, ftol, with_rot, 
     # the reference's objective (with_rot = 2: |[p* - p; rpy* - rpy]|^2, src/inverse_kinematics.jl:38-50)
     kw = dict(lam=lam, tol_pos=0.0, tol_rot=0.0, max_step=max_step, with_rot=2 if with_rot else 0)
 
-    def state(k):  # the iterate after k DLS steps from Q0 (one launch; the active set lives in the kernel)
-        Q = torch.empty_like(Q0)
-        _, _, err = plan.ik_dls(tgt, Q, max_iters=k, Q0=Q0, **kw)
-        return Q, err[:, 0]
-
-    # the iterates k, k + 1, ... are launched 8 at a time and read back with one synchronisation (a
-    # launch of k steps is a few microseconds of one lane: the host round trips dominate, not the steps)
-    Q, e0 = state(0)
-    e0 = e0.cpu().numpy()
-    f = float(e0[0] ** 2 + e0[1] ** 2)
-    status = ":MAXEVAL_REACHED"
-    k = 1
-    while k <= int(max_iters) and status != ":FTOL_REACHED":
-        batch = [state(kk) for kk in range(k, min(k + 8, int(max_iters) + 1))]
-        es = torch.stack([e for _, e in batch]).cpu().numpy()
-        for (Qn, _), e in zip(batch, es):
-            Q = Qn
-            f_new = float(e[0] ** 2 + e[1] ** 2)
-            if abs(f - f_new) < ftol:
-                status = ":FTOL_REACHED"
-                break
-            f = f_new
-        k += len(batch)
+    # every iterate's objective from one launch of max_iters steps (kin_ik_dls_batch_trace), then the
+    # stopping iterate k from a launch of k steps: O(max_iters) steps (the active set the
+    # solver carries between steps lives inside the kernel, so an iterate is a launch from Q0)
+    M = int(max_iters)
+    _, _, tr = plan.ik_dls_trace(tgt, Q0, max_iters=M, **kw)
+    tr = tr[:, :, 0].double().cpu().numpy()
+    f = tr[:, 0] ** 2 + tr[:, 1] ** 2  # f_objective |[p* - p; rpy* - rpy]|^2 of iterates 0 .. M
+    status, k = ":MAXEVAL_REACHED", M
+    for kk in range(1, M + 1):
+        if abs(f[kk - 1] - f[kk]) < ftol:
+            status, k = ":FTOL_REACHED", kk
+            break
+    Q = torch.empty_like(Q0)
+    plan.ik_dls(tgt, Q, max_iters=k, Q0=Q0, **kw)
     q = Q[:, 0].cpu().numpy()
     m.set_joint_angles(joints, q)
     return q, status

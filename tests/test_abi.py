@@ -34,7 +34,7 @@ def test_exports_every_declared_symbol():
     missing = [s for s in decl if not hasattr(L, s)]
     assert not missing, missing
     assert sorted(K.EXPORTS) == decl
-    assert L.kin_abi_version() == 1
+    assert L.kin_abi_version() == 2
     mc, mj, ms = C.c_int32(), C.c_int32(), C.c_int32()
     assert L.kin_limits(C.byref(mc), C.byref(mj), C.byref(ms)) == 0
     assert (mc.value, mj.value, ms.value) == (32, 64, 8)

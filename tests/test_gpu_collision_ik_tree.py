@@ -315,3 +315,137 @@ def test_padded_ldq_beyond_the_narrow_bound():
     got = plan.ik_coll(sdf, tgt, big[:, :N], Q0=big0[:, :N], **KW)
     assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]) and torch.equal(got[2], ref[2])
     del big, big0
+
+
+# ---- the reference's own PR2 shape: both arms (14 joints) + the planar base = 17 variables ----
+
+def _pr2_scene(with_base=True):
+    """tests/golden/pr2_two_arms.urdf at reset_manip_pose (src/models.jl:59-70): the torso (not a batch
+    column) at 0.3; q columns = rarm_joints then larm_joints (test_inverse_kinematics.jl:33, 60)."""
+    names = kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS
+    sc = Scene(golden("pr2_two_arms.urdf"), names, kinhip.PR2_ARM_SPHERES, with_base=with_base)
+    torso = sc.m.find_joint("torso_lift_joint")
+    base = [0.0, 0.0, 0.0] if with_base else []
+    sc.m.set_joint_angles([torso], [0.3] + base)
+    sc.om.set_joint_angles([sc.tree.joint_id("torso_lift_joint")], [0.3] + base)
+    r, l, _ = kinhip.PR2_MANIP_POSE
+    q0 = np.deg2rad(np.array(r + l))
+    if with_base:
+        q0 = np.concatenate([q0, np.zeros(3)])
+    return sc, q0
+
+
+def _pr2_fridge_targets(rng, N):
+    """test_inverse_kinematics.jl:67-68: Transform((0, 0, 1.2)) * pose_fridge (fridge base at (1.2, 0, 0)),
+    perturbed per target."""
+    tg = np.zeros((12, N))
+    for k in range(N):
+        tg[:, k] = _col(_pose((1.2 + rng.uniform(-0.06, 0.0), rng.uniform(-0.06, 0.06), 1.2 + rng.uniform(-0.05, 0.05)),
+                              rng.uniform(-0.2, 0.2)))
+    return tg
+
+
+def test_pr2_plan_accepts_seventeen_variables():
+    """kin_coll_ik_plan_create takes the reference's call shape: 14 arm joints + base = 17 variables (the
+    cap was 12), every sphere of both arms' collision links; the fp32 and fp64 plans specialise."""
+    sc, _ = _pr2_scene()
+    for dt in (torch.float32, torch.float64):
+        plan = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link("l_gripper_tool_frame"), sc.q, dtype=dt)
+        assert plan.n_qcols == 17
+        plan.specialize()
+        assert plan.specialized & kinhip.KIN_SPEC_IK_COLL_SCENE
+
+
+@pytest.mark.parametrize("spec,lanes", [(False, 0), (True, 0), (True, 1), (True, 64)])
+def test_pr2_two_arms_with_base_door_per_target(spec, lanes):
+    """The reference's collision-aware IK call (test/test_inverse_kinematics.jl:52-86, fridge_demo.jl:13-37):
+    PR2 with its base, joints = vcat(rarm, larm), spheres on both arms' collision links, the l_gripper_tool_frame
+    target inside the fridge -- and the fridge door angle per target (kin_ik_coll_batch_scene, the fridge as a
+    UnionSDF attached to its mechanism).  fp64 vs the oracle's or_ik_coll_batch over the static union of each
+    target's fridge state: equal iteration counts, angles 1e-7."""
+    import oracle as O
+    sc, q0 = _pr2_scene()
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(67)
+    N = 128
+    tg = _pr2_fridge_targets(rng, N)
+    link = "l_gripper_tool_frame"
+    plan = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link(link), sc.q, dtype=torch.float64)
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    Q0 = torch.tensor(np.repeat(q0[:, None], N, 1), dtype=torch.float64, device=dev).contiguous()
+    Q1 = torch.empty_like(Q0)
+    plan.ik_dls(tgt, Q1, Q0=Q0, max_iters=64, restarts=3, seed=2, with_rot=2)  # stage 1 (rarm columns pass through)
+    Q1[:7] = Q0[:7]
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    doors = rng.uniform(1.6, 2.4, N)
+    scene_q = torch.tensor(np.stack([doors, np.full(N, 1.2), np.zeros(N), np.zeros(N)]), dtype=torch.float64,
+                           device=dev).contiguous()
+    ft = O.parse_urdf_tree(golden("fridge.urdf"))
+    boxes = [O.OracleUnionSDF(*O.fridge_boxes(ft, door_angle=d, base=(1.2, 0.0, 0.0))) for d in doors]
+    Q, it, err = sc.check(link, tg, Q1, asdf, box=None, boxes=boxes, spec=spec, lanes=lanes, scene_q=scene_q)
+    conv = it <= KW["max_iters"]
+    # the reference's acceptance on the converged targets: |dp| < 1e-3 and every sphere clear (vals > -1e-5)
+    e = err.cpu().numpy()
+    assert (e[0][conv] < 1e-3).all() and (e[2][conv] > KW["margin"] - 1e-5).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_scene_specialized_equals_generic(dtype):
+    """kin_ik_coll_batch_scene's specialised S x G-lane kernels (KIN_SPEC_IK_COLL_SCENE) against the generic
+    kernel: bit-identical angles, iteration counts and errors for every lane layout (the fridge door per
+    target, Fetch's arm)."""
+    sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(71)
+    N = 700
+    tg = _fridge_targets(rng, N)
+    Q1 = _stage1(sc, "gripper_link", tg, dev).to(dtype)
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    scene_q = torch.tensor(np.stack([rng.uniform(1.5, 2.4, N), np.full(N, 1.2), np.zeros(N), np.zeros(N)]),
+                           dtype=dtype, device=dev).contiguous()
+    tgt = torch.tensor(tg, dtype=dtype, device=dev).contiguous()
+    gen = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link("gripper_link"), sc.q, dtype=dtype)
+    spc = kinhip.CollisionIKPlan(sc.sscc, sc.m.find_link("gripper_link"), sc.q, dtype=dtype).specialize()
+    kw = dict(KW, restarts=3)
+    ref = gen.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q, lanes=1, **kw)
+    it = ref[1].cpu().numpy()
+    assert (it <= kw["max_iters"]).mean() > 0.5
+    for lanes in (0, 1, 4, 16, 64):
+        got = spc.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q, lanes=lanes, **kw)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), lanes
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("with_rot", [0, 2])
+def test_pr2_dls_no_collision_vs_oracle(with_base, with_rot):
+    """The reference's "no collision" PR2 case (test/test_inverse_kinematics.jl:29-49): kin_ik_dls_batch over
+    joints = vcat(rarm, larm) (the right arm's 7 columns cannot move l_gripper_tool_frame: left untouched) with
+    and without the base, from reset_manip_pose towards (0.6, 0.7, 0.8) (perturbed per target), position only and
+    the reference's rpy objective.  fp64 iterates vs the oracle's or_ik_dls_batch (equal iteration counts, angles
+    1e-7) and the reference's acceptance |dp| < 1e-3 on the converged targets."""
+    sc, q0 = _pr2_scene(with_base)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(73)
+    N = 256
+    tg = np.zeros((12, N))
+    for k in range(N):
+        tg[:, k] = _col(_pose((0.6 + rng.uniform(-0.05, 0.05), 0.7 + rng.uniform(-0.05, 0.05),
+                               0.8 + rng.uniform(-0.05, 0.05)), rng.uniform(-0.2, 0.2)))
+    link = sc.m.find_link("l_gripper_tool_frame")
+    plan = sc.m.plan(sc.q, out_links=[link], jac_link=link, dtype=torch.float64)
+    tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    Q = torch.tensor(np.repeat(q0[:, None], N, 1), dtype=torch.float64, device=dev).contiguous()
+    kw = dict(max_iters=64, restarts=3, seed=9, lam=1e-2, tol_pos=1e-4, tol_rot=1e-4, max_step=0.5)
+    Q, it, err = plan.ik_dls(tgt, Q, with_rot=with_rot, **kw)
+    rq, rit, rerr = sc.om.ik_dls_batch(np.repeat(q0[:, None], N, 1), sc.ids, sc.tree.link_id("l_gripper_tool_frame"),
+                                       tg, with_rot=with_rot, **kw)
+    it = it.cpu().numpy()
+    np.testing.assert_array_equal(it, rit)
+    np.testing.assert_allclose(Q.cpu().numpy(), rq, atol=1e-7)
+    conv = it <= kw["max_iters"]
+    assert conv.mean() > 0.9, conv.mean()
+    assert (err.cpu().numpy()[0][conv] < 1e-3).all()
+    np.testing.assert_array_equal(Q.cpu().numpy()[:7], np.repeat(q0[:7, None], N, 1))  # the right arm untouched

@@ -207,3 +207,98 @@ def test_shim_sequence_follows_the_mechanism(follow):
     # tree query after add_new_link fails on the stale C model
     if not follow:
         assert any(stale)
+
+
+def test_shim_collision_ik_with_attached_fridge():
+    """KinematicsHIP.jl's inverse_kinematics!(hm, link, joints, targets, Q0, sscc, sdf::HIPSDF; scene_q) with
+    the reference's UnionSDF(fridge) (test/test_inverse_kinematics.jl:52-86, fridge_demo.jl:13-37): the shim's
+    exact C-ABI sequence -- HIPSDF(fridge, [door_joint]) = kin_model_create + kin_sdf_create_attached;
+    the cached plan = kin_coll_ik_plan_create + kin_plan_specialize(0); stage 1 kin_ik_dls_batch_from; stage 2
+    kin_ik_coll_batch_scene with one door angle per target (scene columns door, base x, y, theta) -- replayed
+    through ctypes with the shim's default keywords, against the oracle: stage 1 or_ik_dls_batch, stage 2
+    or_ik_coll_batch over each target's static fridge union (fp64, equal iteration counts, angles 1e-7)."""
+    import oracle as O
+    from kinhip import collision as KC
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    dev = torch.device("cuda", 0)
+    # the robot (Fetch, arm spheres) and the scene: HIPModel(robot), HIPSDF(fridge, [door_joint])
+    m = kinhip.parse_urdf(golden("fetch.urdf"))
+    sscc = kinhip.SweptSphereCollisionChecker(m)
+    kinhip.add_fetch_arm_spheres(sscc)
+    arm = [m.find_joint(n) for n in ARM]
+    gl = m.find_link("gripper_link")
+    m._sync_angles()
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    fr._sync_angles()
+    links = [l for l in fr.links if l.geometric_meta_data is not None and hasattr(l.geometric_meta_data, "extents")]
+    jids = np.array([fr.find_joint("door_joint").id], np.int32)
+    lids = np.array([l.id for l in links], np.int32)
+    org = np.ascontiguousarray(np.array([np.asarray(l.geometric_meta_data.origin, np.float64).T.reshape(16)
+                                         for l in links]).reshape(-1))
+    wid = np.ascontiguousarray(np.array([l.geometric_meta_data.extents for l in links], np.float64).reshape(-1))
+    sdf = C.c_void_p()
+    K.check(K.lib().kin_sdf_create_attached(fr._model, 1, _p(jids), lids.size, _p(lids), _p(org), _p(wid),
+                                            C.byref(sdf)))
+    # cached_plan!: kin_coll_ik_plan_create(KinCollDesc(Float64, ids, sphere links, radii)) + specialise (0)
+    ids = np.array([j.id for j in arm], np.int32)
+    sph = np.array([l.id for l in sscc.sphere_links], np.int32)
+    rad = np.asarray(sscc.sphere_radii, np.float64)
+    d = K.CollDesc(K.KIN_F64, ids.size, _p(ids).value, sph.size, _p(sph).value, None, _p(rad).value)
+    p = C.c_void_p()
+    K.check(K.lib().kin_coll_ik_plan_create(m._model, C.byref(d), gl.id, C.byref(p)))
+    K.check(K.lib().kin_plan_specialize(p, 0))
+    N = 160
+    rng = np.random.default_rng(79)
+    tg = np.zeros((12, N))
+    for k in range(N):
+        T = np.eye(4)
+        c, s = np.cos(rng.uniform(-0.3, 0.3)), np.sin(rng.uniform(-0.3, 0.3))
+        T[:3, :3] = [[c, -s, 0], [s, c, 0], [0, 0, 1]]
+        T[:3, 3] = (rng.uniform(0.9, 1.05), rng.uniform(-0.12, 0.12), rng.uniform(1.15, 1.32))
+        tg[:, k] = np.concatenate([T[:3, :3].T.reshape(-1), T[:3, 3]])
+    doors = rng.uniform(1.5, 2.4, N)
+    targets = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
+    scene_q = torch.tensor(np.stack([doors, np.full(N, 1.2), np.zeros(N), np.zeros(N)]), dtype=torch.float64,
+                           device=dev).contiguous()
+    Q0 = torch.zeros((8, N), dtype=torch.float64, device=dev)
+    Q1, Q = torch.empty_like(Q0), torch.empty_like(Q0)
+    iters = torch.empty(N, dtype=torch.int32, device=dev)
+    err = torch.empty((3, N), dtype=torch.float64, device=dev)
+    # the shim's defaults: max_iters=64, lambda=1e-2, tol 1e-3, max_step=0.5, rpy_objective -> with_rot 2,
+    # restarts=3, seed=0, lanes=0, damp_err=0; margin=0.02, band=0, weight=1, feas=1e-6
+    prm = K.IkParams(64, 1e-2, 1e-3, 1e-3, 0.5, 2, 3, 0, 0, 0)
+    cp = K.IkCollParams(0.02, 0.0, 1.0, 1e-6)
+    try:
+        K.check(K.lib().kin_ik_dls_batch_from(p, C.byref(prm), targets.data_ptr(), N, Q0.data_ptr(), Q1.data_ptr(),
+                                              N, N, iters.data_ptr(), err.data_ptr(), N, None))
+        K.check(K.lib().kin_ik_coll_batch_scene(p, sdf, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                                scene_q.data_ptr(), N, Q1.data_ptr(), Q.data_ptr(), N, N,
+                                                iters.data_ptr(), err.data_ptr(), N, None))
+        torch.cuda.synchronize()
+    finally:
+        K.lib().kin_plan_destroy(p)
+        K.lib().kin_sdf_destroy(sdf)
+    tree = O.parse_urdf_tree(golden("fetch.urdf"))
+    om = O.OracleMech(tree)
+    osph, opar = [], []
+    for name, c, _ in KC.FETCH_ARM_SPHERES:
+        T = np.eye(4)
+        T[:3, 3] = c
+        osph.append(om.add_new_link(tree.link_id(name), T))
+        opar.append(tree.link_id(name))
+    oids = [tree.joint_id(n) for n in ARM]
+    kw = dict(max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3, max_step=0.5, with_rot=2, restarts=3, seed=0)
+    q1, _, _ = om.ik_dls_batch(np.zeros((8, N)), oids, tree.link_id("gripper_link"), tg, **kw)
+    np.testing.assert_allclose(Q1.cpu().numpy(), q1, atol=1e-7)
+    ft = O.parse_urdf_tree(golden("fridge.urdf"))
+    boxes = [O.OracleUnionSDF(*O.fridge_boxes(ft, door_angle=dd, base=(1.2, 0.0, 0.0))) for dd in doors]
+    rq, rit, rerr = O.ik_coll_batch(om, None, q1, oids, tree.link_id("gripper_link"), tg, osph, list(rad),
+                                    margin=0.02, band=0.0, weight=1.0, feas=1e-6, sdfs=boxes, sphere_parents=opar, **kw)
+    it = iters.cpu().numpy()
+    same = it == rit
+    assert (~same).mean() <= 0.01, (np.where(~same)[0], it[~same], rit[~same])
+    c = same & (it <= 64)
+    assert c.mean() > 0.8
+    np.testing.assert_allclose(Q.cpu().numpy()[:, c], rq[:, c], atol=1e-7)
+    np.testing.assert_allclose(err.cpu().numpy()[:, c], rerr[:, c], atol=1e-9)

@@ -779,6 +779,31 @@ def test_ik_reference_target(dev):
         np.testing.assert_allclose(kinhip.rpy(Tn), kinhip.rpy(T), atol=1e-3)
 
 
+@pytest.mark.parametrize("spec", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_ik_trace_equals_separate_launches(dev, fetch_tree, spec, dtype):
+    """kin_ik_dls_batch_trace (the ftol_abs rule's one launch): row k of the trace is
+    bit for bit the err of a separate launch of k steps from the same seeds, for every k (restarts = 0: the
+    attempt length depends on max_iters); the final angles and iteration counts equal an ordinary launch's."""
+    m, arm = _fetch(False)
+    gl = m.find_link("gripper_link")
+    om = O.OracleMech(fetch_tree)
+    N = 300
+    tgt = _targets(om, [j.id for j in arm], gl.id, N, 45)
+    T = torch.tensor(tgt, dtype=dtype, device=dev).contiguous()
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dtype)
+    if spec:
+        plan.specialize(kinhip.KIN_SPEC_IK)
+    Q0 = torch.zeros((8, N), dtype=dtype, device=dev)
+    kw = dict(lam=1e-2, tol_pos=0.0, tol_rot=0.0, max_step=0.5, with_rot=2, restarts=0, seed=3)
+    M = 12
+    Qt, itt, tr = plan.ik_dls_trace(T, Q0, max_iters=M, **kw)
+    for k in range(M + 1):
+        Q, it, err = plan.ik_dls(T, torch.empty_like(Q0), Q0=Q0, max_iters=k, lanes=1, **kw)
+        assert torch.equal(tr[k], err), k
+    assert torch.equal(Qt, Q) and torch.equal(itt, it)
+
+
 # ------------------------------------------------------- plan specialisation ---
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("with_base", [False, True])

@@ -1,0 +1,65 @@
+"""Two host threads on hipStreamPerThread: the handle ((hipStream_t)2) names each calling
+thread's own default stream, so the two-phase IK's "same stream as last time" shortcut must not hand one
+thread's in-flight scratch set (hand-over rings, fail lists) to the other.  Both threads run config-4 sized
+batches (two-phase schedule) back to back on that handle, each into its own outputs; every result must
+equal the single-threaded reference bit for bit."""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ARM, golden
+
+import kinhip
+from kinhip import _lib as K
+
+pytestmark = pytest.mark.gpu
+
+HIP_STREAM_PER_THREAD = C.c_void_p(2)
+
+
+def test_two_threads_on_the_per_thread_stream_handle():
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    dev = torch.device("cuda", 0)
+    m = kinhip.parse_urdf(golden("fetch.urdf"))
+    arm = [m.find_joint(n) for n in ARM]
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32).specialize()
+    N = 65536  # more than one round of waves: the two-phase schedule and its scratch sets
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=31,
+                                dtype=torch.float32, device=dev)
+    tgt = plan.run(Qt)[0][0].contiguous()
+    Q0 = torch.zeros((8, N), dtype=torch.float32, device=dev)
+    kw = dict(max_iters=64, restarts=3, seed=0, lam=1e-2, max_step=0.5, tol_pos=1e-3, tol_rot=1e-3)
+    ref_q, ref_it, _ = plan.ik_dls(tgt, torch.empty_like(Q0), Q0=Q0, **kw)
+    torch.cuda.synchronize()
+    prm = K.IkParams(64, 1e-2, 1e-3, 1e-3, 0.5, 1, 3, 0, 0, 0)
+    reps = 6
+    outs = [[(torch.empty_like(Q0), torch.empty(N, dtype=torch.int32, device=dev)) for _ in range(reps)]
+            for _ in range(2)]
+    errors = []
+    barrier = threading.Barrier(2)
+
+    def worker(t):
+        try:
+            torch.cuda.set_device(dev)
+            barrier.wait()
+            for Q, it in outs[t]:
+                K.check(K.lib().kin_ik_dls_batch_from(plan._h, C.byref(prm), tgt.data_ptr(), N, Q0.data_ptr(),
+                                                      Q.data_ptr(), N, N, it.data_ptr(), None, N,
+                                                      HIP_STREAM_PER_THREAD))
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for t in range(2):
+        for Q, it in outs[t]:
+            assert torch.equal(it, ref_it) and torch.equal(Q, ref_q), t

@@ -4,6 +4,9 @@
 #   gpurun -- bash tools/gpu_session.sh <step> [<step> ...]
 # steps:
 #   tests[=<pytest selection>]  the GPU suite (default: tests/), -x, per-test timeout
+#   alltests=<pytest selection> the same without -x (every failure of a new batch of tests in one call)
+#   isa                         the bench on the A/B build with KINHIP_JIT_CODE_DUMP (every specialised code object
+#                               the bench compiles) + tools/isa_check.py over them and the generic kernels
 #   smoke                       __graft_entry__.smoke()
 #   bench                       python bench.py -> gpurun_out/bench.json
 #   bench-trace                 rocprofv3 --kernel-trace --stats of `bench.py --no-cpu` (gpurun_out/prof/bench)
@@ -42,6 +45,18 @@ for step in "$@"; do
         > gpurun_out/gpu_tests.log 2>&1
       rc=$?; tail -3 gpurun_out/gpu_tests.log
       [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/gpu_tests.log | head -30; exit $rc; } ;;
+    alltests=*)
+      sel=${step#alltests=}
+      timeout -k 10 1500 python -u -m pytest $sel -m gpu -v --timeout 300 --timeout-method thread \
+        > gpurun_out/gpu_tests_all.log 2>&1
+      rc=$?; tail -3 gpurun_out/gpu_tests_all.log
+      [ $rc -eq 0 ] || grep -E "FAILED|Error" gpurun_out/gpu_tests_all.log | head -30 ;;
+    isa)
+      mkdir -p gpurun_out/isa
+      timeout -k 10 400 env KINHIP_LIB=$AB KINHIP_JIT_CODE_DUMP=$PWD/gpurun_out/isa/jit python bench.py --no-cpu \
+        > gpurun_out/isa/bench_ab.json 2> gpurun_out/isa/bench_ab.err || { tail gpurun_out/isa/bench_ab.err; exit 9; }
+      python tools/isa_check.py gpurun_out/isa/jit.*.co > gpurun_out/isa/isa_check.txt 2>&1; tail -3 gpurun_out/isa/isa_check.txt
+      rm -f gpurun_out/isa/jit.*.co ;;
     smoke)
       timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | quiet || exit 2 ;;
     bench)
