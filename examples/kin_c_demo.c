@@ -23,6 +23,10 @@
     } while (0)
 
 int main(int argc, char** argv) {
+    if (kin_abi_version() != KINHIP_ABI_VERSION) {  /* the kin_* structs this file was compiled against */
+        fprintf(stderr, "libkinhip C-ABI version %d, this program needs %d\n", kin_abi_version(), KINHIP_ABI_VERSION);
+        return 1;
+    }
     const char* urdf = argc > 1 ? argv[1] : "tests/golden/fetch.urdf";
     const char* arm[8] = {"torso_lift_joint", "shoulder_pan_joint", "shoulder_lift_joint", "upperarm_roll_joint",
                           "elbow_flex_joint", "forearm_roll_joint", "wrist_flex_joint", "wrist_roll_joint"};

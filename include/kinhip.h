@@ -53,8 +53,9 @@ extern "C" {
 
 #define KINHIP_API __attribute__((visibility("default")))
 /* ABI version (kin_abi_version): 2 since kin_ik_params gained damp_err (round 4) -- a caller built against
- * version 1 passes a shorter kin_ik_params, so bindings check this value at load (the Python mirror and
- * the Julia shim refuse a mismatch) and the library's soname is libkinhip.so.2. */
+ * version 1 passes a shorter kin_ik_params, so every binding checks kin_abi_version() == KINHIP_ABI_VERSION
+ * before its first call (the Python mirror, the Julia shim and examples/kin_c_demo.c refuse a mismatch;
+ * INTEGRATION.md). */
 #define KINHIP_ABI_VERSION 2
 
 typedef enum {

@@ -24,6 +24,31 @@
 #define KIN_IKT_UNROLL
 #endif
 
+// Diagnostic section stamps (tools only: KINHIP_JIT_DEFS=-DKINHIP_IKT_SECT=<k> in the A/B build,
+// tools/ikt_sect.py): the cycles of iteration section k (1 tree walk, 2 sphere distances + rows, 3 rows into
+// the normal equations, 4 pose error + checks, 5 pose rows, 6 factorisation + solves, 7 step + loop top)
+// summed over the writer lane's iterations replace err row 0, its cycles from the first iteration to the
+// write err row 1.  Never in a product build.
+#ifndef KINHIP_IKT_SECT
+#define KINHIP_IKT_SECT 0
+#endif
+#if KINHIP_IKT_SECT
+#define KIN_IKT_STAMP(k)                                                   \
+    do {                                                                   \
+        uint64_t t_;                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        if ((k) == KINHIP_IKT_SECT) sect_acc += t_ - sect_prev;            \
+        sect_prev = t_;                                                    \
+        if (sect_t0 == 0) sect_t0 = t_;                                    \
+    } while (0)
+#else
+#define KIN_IKT_STAMP(k) \
+    do {                 \
+    } while (0)
+#endif
+
 namespace kinhip {
 namespace {
 
@@ -275,6 +300,9 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
     T ep = T(0), er = T(0), dmin = T(INFINITY);
     const T w2 = cz.weight * cz.weight;
     const T act = cz.margin + cz.band;
+#if KINHIP_IKT_SECT
+    uint64_t sect_acc = 0, sect_prev = 0, sect_t0 = 0;
+#endif
     const uint32_t active = P.free_mask;
     auto sdf_at = [&](T px, T py, T pz, T& d, T (&g)[3]) {  // the union (static or attached) at one point
         T xs[1] = {px}, ys[1] = {py}, zs[1] = {pz}, ds[1], gs[1][3];
@@ -294,6 +322,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             if (done) break;
         }
         if (done) continue;
+        KIN_IKT_STAMP(7);
         // ---- tree walk: frames, joint records, spheres ----------------------------------------------
         Fr<T> root;
         if (base) base_frame(root, b[0], b[1], b[2]);
@@ -381,6 +410,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             if (s == P.tgt_step) Lf = cur;
         }
         link_frame(Lf, Lf, P.has_xt != 0, P.Xt);
+        KIN_IKT_STAMP(1);
         if constexpr (S > 1) {
             // this lane's spheres: distance, gradient, row; then every in-band row into the system in
             // sphere order, broadcast from its lane
@@ -400,6 +430,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 inband[r] = __ballot(inb);
             }
             dmin = row_group_min<S>(dl);
+            KIN_IKT_STAMP(2);
             KIN_IKT_UNROLL
             for (int k = 0; k < P.n_sph; ++k) {
                 const int r = k / S, src = gbase + k % S;
@@ -423,6 +454,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 }
             }
         }
+        KIN_IKT_STAMP(3);
         // ---- pose error, convergence, attempt ends ---------------------------------------------------
         T e[6];
         e[0] = pt[0] - Lf.t[0]; e[1] = pt[1] - Lf.t[1]; e[2] = pt[2] - Lf.t[2];
@@ -477,6 +509,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             held = 0;
             continue;
         }
+        KIN_IKT_STAMP(4);
         // ---- pose rows: J^T J and J^T e ---------------------------------------------------------------
         // row r of J over the variables: revolute [z x p - m; z], prismatic [z; 0], base [1 0 -y'; 0 1 x'; ..]
         // (p' = p - base); with the reference objective the angular rows are d(rpy)/dq.  Accumulated row by
@@ -516,6 +549,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                     if ((P.tgt_mask >> c) & 1u) A[v][c] = fma(Jr[v], Jr[c], A[v][c]);
             }
         }
+        KIN_IKT_STAMP(5);
         // ---- the step --------------------------------------------------------------------------------
         const uint32_t freev = active & ~held;
 #pragma unroll
@@ -572,6 +606,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             if constexpr (fast) y[r] = sm * ip[r];
             else y[r] = sm / A[r][r];
         }
+        KIN_IKT_STAMP(6);
         T mx = T(0);
         uint32_t nh = 0;
 #pragma unroll
@@ -624,6 +659,14 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
     if (base)
         for (int k = 0; k < 3; ++k) st_soa(q, P.base_col + k, ldq, off, b[k]);
     if (iters) iters[gi] = conv ? it : a.max_iters + 1;
+#if KINHIP_IKT_SECT
+    {
+        uint64_t t_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        ep = (T)(double)sect_acc;
+        er = (T)(double)(t_ - sect_t0);
+    }
+#endif
     if (err) {
         st_soa(err, 0, lde, off, ep);
         st_soa(err, 1, lde, off, er);

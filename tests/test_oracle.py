@@ -58,6 +58,38 @@ def test_ground_truth_fk(gt, pr2, with_base):
 
 
 @pytest.mark.parametrize("with_base", [False, True])
+def test_pr2_two_arms_fixture_ground_truth(gt, with_base):
+    """tests/golden/pr2_two_arms.urdf (the two-arm PR2 of the round-5 collision-IK tests) carries the chain
+    data/ground_truth.json pins: its link poses at the fixture's angles equal the reference's to 1e-12, and
+    the mirrored left arm is the right arm reflected in the x-z plane (y -> -y) at mirrored angles."""
+    t = O.parse_urdf_tree(golden("pr2_two_arms.urdf"))
+    m = O.OracleMech(t, with_base=with_base)
+    jids = [t.joint_id(n) for n in gt["joint_names"]]
+    base = [0.3, 0.3, 0.3] if with_base else []
+    m.set_joint_angles(jids, list(gt["angle_vector"]) + base)
+    for ln, pg in zip(gt["link_names"], gt["pose_list"]):
+        T = m.get_transform(t.link_id(ln))
+        pg = np.asarray(pg)
+        if with_base:
+            np.testing.assert_allclose(T[:3, 3], _rotz(0.3) @ pg[:3] + [0.3, 0.3, 0], atol=1e-12)
+        else:
+            np.testing.assert_allclose(T[:3, 3], pg[:3], atol=1e-12)
+    # mirror: pan / roll joints (axes z, x) flip sign, the lift / flex joints (axis y) keep theirs
+    m2 = O.OracleMech(t)
+    rng = np.random.default_rng(3)
+    names = ["shoulder_pan_joint", "shoulder_lift_joint", "upper_arm_roll_joint", "elbow_flex_joint",
+             "forearm_roll_joint", "wrist_flex_joint", "wrist_roll_joint"]
+    sign = np.array([-1, 1, -1, 1, -1, 1, -1.0])
+    for _ in range(5):
+        q = rng.uniform(-1, 0, 7)
+        m2.set_joint_angles([t.joint_id("r_" + n) for n in names] + [t.joint_id("l_" + n) for n in names],
+                            list(q) + list(sign * q))
+        Tr = m2.get_transform(t.link_id("r_gripper_tool_frame"))
+        Tl = m2.get_transform(t.link_id("l_gripper_tool_frame"))
+        np.testing.assert_allclose(Tl[:3, 3], Tr[:3, 3] * [1, -1, 1], atol=1e-12)
+
+
+@pytest.mark.parametrize("with_base", [False, True])
 def test_fd_jacobian_all_links(gt, pr2, with_base):
     """test/test_kinematics.jl:43-73, every link, fixture angles and zeros."""
     m = O.OracleMech(pr2, with_base=with_base)

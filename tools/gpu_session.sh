@@ -17,6 +17,7 @@
 #                               tools/prof_kernel.py (e.g. fkjac32ts, ik32s, coll32s, collg32s, cik32s)
 #   ik                          config-4 IK timing (product, twice) and 1M targets; per-iteration probe
 #   ik-sections                 iteration section stamps (A/B build, -DKINHIP_IK_SECT=k)
+#   ikt-sections                collision-aware IK (f3 stage 2) section stamps (A/B build, -DKINHIP_IKT_SECT=k)
 #   ik-timeline                 per-lane entry / write timeline of one solve (A/B build)
 #   ik-dump                     the specialised IK source (A/B build, KINHIP_JIT_DUMP) + a kernel trace of config 4
 #   coll                        the plain-row padding A/B of the config-5 legs (tools/coll_pad_ab.py)
@@ -53,10 +54,9 @@ for step in "$@"; do
       [ $rc -eq 0 ] || grep -E "FAILED|Error" gpurun_out/gpu_tests_all.log | head -30 ;;
     isa)
       mkdir -p gpurun_out/isa
-      timeout -k 10 400 env KINHIP_LIB=$AB KINHIP_JIT_CODE_DUMP=$PWD/gpurun_out/isa/jit python bench.py --no-cpu \
-        > gpurun_out/isa/bench_ab.json 2> gpurun_out/isa/bench_ab.err || { tail gpurun_out/isa/bench_ab.err; exit 9; }
-      python tools/isa_check.py gpurun_out/isa/jit.*.co > gpurun_out/isa/isa_check.txt 2>&1; tail -3 gpurun_out/isa/isa_check.txt
-      rm -f gpurun_out/isa/jit.*.co ;;
+      timeout -k 10 400 env KINHIP_LIB=$AB KINHIP_JIT_CODE_DUMP=$PWD/gpurun_out/isa/jit KINHIP_JIT_DUMP=$PWD/gpurun_out/isa/src \
+        python bench.py --no-cpu > gpurun_out/isa/bench_ab.json 2> gpurun_out/isa/bench_ab.err || { tail gpurun_out/isa/bench_ab.err; exit 9; }
+      python tools/isa_check.py gpurun_out/isa/jit.*.co > gpurun_out/isa/isa_check.txt 2>&1; tail -3 gpurun_out/isa/isa_check.txt ;;
     smoke)
       timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | quiet || exit 2 ;;
     bench)
@@ -99,6 +99,10 @@ for step in "$@"; do
     ik-sections)
       for k in 1 2 3 4 5 6 7; do
         timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=$k python -u tools/ik_sect.py 2>&1 | quiet || exit 8
+      done ;;
+    ikt-sections)
+      for k in 1 2 3 4 5 6 7; do
+        timeout -k 10 180 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IKT_SECT=$k python -u tools/ikt_sect.py 2>&1 | quiet || exit 8
       done ;;
     ik-timeline)
       timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=9 python -u tools/ik_timeline.py 2>&1 | quiet || exit 8 ;;
