@@ -182,6 +182,9 @@ __device__ __forceinline__ float atan2_pos_fast(float s, float c) {
     return c < 0.0f ? 3.14159265f - r : r;
 }
 __device__ __forceinline__ double atan2_pos_fast(double s, double c) { return atan2(s, c); }
+// atan2(y, x) over the whole plane (fp32): atan2_pos_fast's octant reduction and polynomial, the sign of y last
+// (max abs error 3.1e-7; atan2(+-0, x < 0) = +-pi as the library's)
+__device__ __forceinline__ float atan2_fast(float y, float x) { return copysignf(atan2_pos_fast(fabsf(y), x), y); }
 
 // SoA addressing: element `row` of a [rows][ld] array for this lane.  Each
 // row gets a wave-uniform buffer descriptor (SGPRs: base = row pointer) and
@@ -401,17 +404,27 @@ __device__ __forceinline__ void motion(Fr<T>& f, int32_t kind, int32_t flags, T 
 // rpy(tf) (src/transform.jl:45-48: RotZYX angles as [roll, pitch, yaw]) of a row-major rotation,
 // and the rpy_derivative! coefficients at it (src/algorithm.jl:56-63, a = -rpy):
 //   d(rpy)/dt = [k0 x + k1 y, k2 x + k3 y, k4 x + k5 y + z] for an angular velocity (x, y, z)
-template <typename T>
+// FAST (the fp32 IK kernels, KINHIP_IK_FAST_ATAN): the polynomial atan2 (atan2_fast, 3.1e-7 abs), the hardware
+// sin / cos (3.6e-7 abs) and v_rcp_f32 in place of atan2f, the reduced sincos and the IEEE division -- inside an
+// iterative solve whose residual is checked against tol_rot (the fp64 kernels keep the exact functions).
+template <bool FAST = false, typename T>
 __device__ __forceinline__ void rpy_and_rate(const T (&r)[9], T (&rpy)[3], T (&k)[6]) {
-    const T t1 = atan2_t(r[3], r[0]);
+    constexpr bool F = FAST && sizeof(T) == 4;
+    auto at2 = [](T y, T x) -> T {
+        if constexpr (F) return atan2_fast(y, x);
+        else return atan2_t(y, x);
+    };
+    const T t1 = at2(r[3], r[0]);
     T s1, c1;
-    sincos_t(t1, &s1, &c1);
-    const T t2 = atan2_t(-r[6], fma(r[3], s1, r[0] * c1));
-    const T t3 = atan2_t(fma(r[2], s1, -(r[5] * c1)), fma(r[4], c1, -(r[1] * s1)));
+    joint_sincos<F>(t1, &s1, &c1);
+    const T t2 = at2(-r[6], fma(r[3], s1, r[0] * c1));
+    const T t3 = at2(fma(r[2], s1, -(r[5] * c1)), fma(r[4], c1, -(r[1] * s1)));
     rpy[0] = t3; rpy[1] = t2; rpy[2] = t1;
     T s2, c2;
-    sincos_t(t2, &s2, &c2);  // a2 = -t2: cos(a2) = c2, sin(a2) = -s2; a3 = -t1: cos = c1, sin = -s1
-    const T ic2 = T(1) / c2;
+    joint_sincos<F>(t2, &s2, &c2);  // a2 = -t2: cos(a2) = c2, sin(a2) = -s2; a3 = -t1: cos = c1, sin = -s1
+    T ic2;
+    if constexpr (F) ic2 = rcp_fast(c2);
+    else ic2 = T(1) / c2;
     k[0] = c1 * ic2; k[1] = s1 * ic2;
     k[2] = -s1; k[3] = c1;
     k[4] = c1 * s2 * ic2; k[5] = s1 * s2 * ic2;

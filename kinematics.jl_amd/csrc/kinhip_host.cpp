@@ -1649,6 +1649,14 @@ int stage_ikc_tree(const kin_model& m, const kin_coll_desc* c, int32_t link_id, 
                 K.vlo[qcol[j]] = (T)m.jlo[j];
                 K.vhi[qcol[j]] = (T)m.jhi[j];
             }
+        // the normal equations' structure: entry (v, c) gets terms from the pose rows when both move the
+        // target, from a sphere's row when both move that sphere
+        auto add_block = [&](uint32_t mask) {
+            for (int v = 0; v < nv; ++v)
+                if ((mask >> v) & 1u) K.nzrow[v] |= mask & ((2u << v) - 1u);
+        };
+        add_block(tgt_mask);
+        for (const IkcSphD& sd : spheres) add_block(sd.step < 0 ? base_bits : steps[sd.step].anc);
         for (int32_t s = 0; s < ns; ++s) {
             const IkcStepD& a = steps[s];
             auto& b = st_out[s];

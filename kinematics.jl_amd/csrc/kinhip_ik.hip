@@ -221,8 +221,12 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             // hold never reaches a workgroup that has to wait for a slot.  Round 4 dealt the list over the
             // WHOLE grid (4,096 workgroups at config 4): the fp64 kernel, two resident workgroups per CU,
             // then ran a 1,000-wave list in two rounds of one busy wave per workgroup (config 4 fp64
-            // 0.145 -> 0.365 ms, BENCH_r04; A/B profiles/r05_ik_p2_ab.txt).  Generic kernels: block-major.
-            // KINHIP_IK_P2_SPREAD=<0|1|2 (whole grid)>, KINHIP_IK_P2_BLOCK=<64|256> (A/B build).
+            // 0.145 -> 0.365 ms, BENCH_r04; A/B profiles/r05_ik_p2_ab.txt).  Measured (round 5): the spread
+            // over the resident workgroups helps the fp64 kernel (2 workgroups per CU; damped config 4 0.172 ->
+            // 0.158 ms) and costs the fp32 one (3 per CU: 0.073 -> 0.087 ms; co-resident workgroups stack their
+            // first waves), so it applies to kernels of at most 2 resident workgroups per CU; others and the
+            // generic kernels run block-major (round 3's order).  KINHIP_IK_P2_SPREAD=<0 never | 1 (default) |
+            // 2 always | 3 whole grid (round 4)>, KINHIP_IK_P2_BLOCK=<64|256> (A/B build).
             static const int p2_block_env = ab_env_int("KINHIP_IK_P2_BLOCK", 256);
             static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 1);
             const int bs2 = p2_block_env == 64 ? 64 : 256;
@@ -230,8 +234,9 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             if (spread_env != 0 && bs2 == 256 && jf) {  // (the resident workgroups of the phase-2 kernel)
                 const hipFunction_t f2 = jf->ik[a.with_rot ? 1 : 0][G2 == 1 ? 0 : G2 == 2 ? 1 : G2 == 4 ? 2 : 3];
                 int nb = 0;
-                if (f2 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f2, 256, 0) == hipSuccess && nb > 0)
-                    a2.p2_spread = spread_env == 2 ? (int)(((c + ng2 - 1) / ng2 * 64 + 255) / 256)  // (A/B: whole grid)
+                if (f2 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f2, 256, 0) == hipSuccess && nb > 0 &&
+                    (nb <= 2 || spread_env > 1))
+                    a2.p2_spread = spread_env == 3 ? (int)(((c + ng2 - 1) / ng2 * 64 + 255) / 256)  // (A/B: whole grid)
                                                    : nb * cus;
             }
             a2.fail_ctl = scr.fail_ctl;

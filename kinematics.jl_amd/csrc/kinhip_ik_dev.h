@@ -377,7 +377,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         }
         if (ROWS == 6 && a.rpy_obj) {
             T kk[6];
-            rpy_and_rate(Rt, trpy, kk);
+            rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Rt, trpy, kk);
         }
         b0[0] = b0[1] = b0[2] = T(0);
         if (base)
@@ -533,7 +533,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             T w[3];
             if (a.rpy_obj) {  // wave-uniform
                 T r[3];
-                rpy_and_rate(Lf.r, r, kr);
+                rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Lf.r, r, kr);
 #pragma unroll
                 for (int k = 0; k < 3; ++k) w[k] = wrap_pi(trpy[k] - r[k]);
             } else {

@@ -70,6 +70,23 @@ __device__ __forceinline__ T pick(const T (&a)[N], int i) {
     for (int k = 1; k < N; ++k) v = (i == k) ? a[k] : v;
     return v;
 }
+// a[i] for a per-lane (divergent) index: a binary tree of selects on the bits of i.  (pick's chain of
+// `i == k` selects is recognised as a dynamic vector index, which a divergent index lowers through scratch
+// memory: a store of the whole array and an indexed load per use.)  Indices >= N give a[N - 1].
+template <typename T, int N>
+__device__ __forceinline__ T pick_lane(const T (&a)[N], int i) {
+    constexpr int B = N <= 1 ? 0 : N <= 2 ? 1 : N <= 4 ? 2 : N <= 8 ? 3 : N <= 16 ? 4 : 5;
+    T t[1 << B];
+#pragma unroll
+    for (int k = 0; k < (1 << B); ++k) t[k] = a[k < N ? k : N - 1];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const bool bit = (i >> b) & 1;
+#pragma unroll
+        for (int k = 0; k < (1 << (B - 1 - b)); ++k) t[k] = bit ? t[2 * k + 1] : t[2 * k];
+    }
+    return t[0];
+}
 template <typename T, int N>
 __device__ __forceinline__ void put(T (&a)[N], int i, T v) {
 #pragma unroll
@@ -177,12 +194,19 @@ __device__ __forceinline__ T row_bcast16(T v, int l) {
 #undef KIN_RB
 }
 
-// min over the G attempt groups of a target (lanes S apart): DPP inside a quad for S = 1, else
-// ds_bpermute (once per iteration)
+// min over the G attempt groups of a target (lanes S apart; v uniform inside each group): DPP inside a quad
+// for S = 1; a target that fills the wave (G * S = 64) reads each group's value with v_readlane and takes the
+// minimum in scalar registers (no LDS round trip: two dependent ds_bpermute sat on the one-wave critical path
+// of every iteration); else ds_bpermute
 template <int G, int S>
 __device__ __forceinline__ int attempt_min(int v) {
     if constexpr (S == 1) {
         return group_min<G>(v);
+    } else if constexpr (G * S == 64) {
+        int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+        for (int g = 1; g < G; ++g) m = min(m, __builtin_amdgcn_readlane(v, g * S));
+        return m;
     } else {
 #pragma unroll
         for (int w = S; w < G * S; w <<= 1) v = min(v, __shfl_xor(v, w));
@@ -191,9 +215,16 @@ __device__ __forceinline__ int attempt_min(int v) {
 }
 template <int G, int S, typename T>
 __device__ __forceinline__ T attempt_min_t(T v) {
+    if constexpr (G * S == 64 && S > 1 && sizeof(T) == 4) {
+        float m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
 #pragma unroll
-    for (int w = S; w < G * S; w <<= 1) v = fmin(v, __shfl_xor(v, w));
-    return v;
+        for (int g = 1; g < G; ++g) m = fminf(m, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), g * S)));
+        return m;
+    } else {
+#pragma unroll
+        for (int w = S; w < G * S; w <<= 1) v = fmin(v, __shfl_xor(v, w));
+        return v;
+    }
 }
 
 // starting angles of an attempt: attempt 0 from q0; attempt k >= 1 re-draws every free joint variable
@@ -275,7 +306,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
     }
     if (ROWS == 6 && a.rpy_obj) {
         T kk[6];
-        rpy_and_rate(Rt, trpy, kk);
+        rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Rt, trpy, kk);
     }
     // the scene state of this target (boxes attached to a scene mechanism): fixed during the solve
     constexpr int MG = MAXG > 0 ? MAXG : 1;
@@ -339,6 +370,20 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             bv[r] = T(0);
 #pragma unroll
             for (int c = 0; c < MAXV; ++c) A[r][c] = T(0);
+        }
+        // S > 1: the rows of the normal equations are accumulated by their owners -- lane sl of an attempt group
+        // owns rows v = sl, sl + S, ... (Ao[o] = row o S + sl, bo[o] its right-hand side) -- and gathered into A /
+        // bv for the (replicated) factorisation.  Each entry gets the same FMAs in the same order as the one-lane
+        // kernel (spheres in order, then the pose rows), so the results are bit-identical for every S; a group's
+        // lanes no longer each form every entry (the sphere rows and the pose rows were ~2/3 of the FMAs of an
+        // iteration, on the one-wave critical path of the batch's slowest target).
+        constexpr int NRO = S > 1 ? (MAXV + S - 1) / S : 1;
+        T Ao[NRO][MAXV], bo[NRO];
+#pragma unroll
+        for (int o = 0; o < NRO; ++o) {
+            bo[o] = T(0);
+#pragma unroll
+            for (int c = 0; c < MAXV; ++c) Ao[o][c] = T(0);
         }
         dmin = T(INFINITY);
         // S > 1: this lane's sphere of each round (centre, radius, the variables moving it)
@@ -450,7 +495,18 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
 #pragma unroll
                             for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? bc(av[rr][v]) : T(0);
                         }
-                    accum_row<T, MAXV>(A, bv, ak, vk, w2, anc);
+                    // this lane's rows (accum_row's operations on them)
+#pragma unroll
+                    for (int o = 0; o < NRO; ++o) {
+                        const int v = o * S + sl;
+                        if (v < MAXV && ((anc >> v) & 1u)) {  // (per lane)
+                            const T wr = w2 * pick_lane(ak, v);
+                            bo[o] = fma(wr, vk, bo[o]);
+#pragma unroll
+                            for (int c = 0; c < MAXV; ++c)
+                                if ((anc >> c) & 1u) Ao[o][c] = fma(wr, ak[c], Ao[o][c]);
+                        }
+                    }
                 }
             }
         }
@@ -465,7 +521,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             T w[3];
             if (a.rpy_obj) {
                 T r[3];
-                rpy_and_rate(Lf.r, r, kr);
+                rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Lf.r, r, kr);
 #pragma unroll
                 for (int k = 0; k < 3; ++k) w[k] = wrap_pi(trpy[k] - r[k]);
             } else {
@@ -540,13 +596,38 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                                                                             : fma(kr[4], x, fma(kr[5], y, z));
                 else Jr[v] = r == 3 ? x : r == 4 ? y : z;
             }
+            if constexpr (S > 1) {  // the owned rows
+#pragma unroll
+                for (int o = 0; o < NRO; ++o) {
+                    const int v = o * S + sl;
+                    if (v < MAXV && ((P.tgt_mask >> v) & 1u)) {  // (per lane)
+                        const T jv = pick_lane(Jr, v);
+                        bo[o] = fma(jv, e[r], bo[o]);
+#pragma unroll
+                        for (int c = 0; c < MAXV; ++c)
+                            if ((P.tgt_mask >> c) & 1u) Ao[o][c] = fma(jv, Jr[c], Ao[o][c]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int v = 0; v < MAXV; ++v) {
+                    if (!((P.tgt_mask >> v) & 1u)) continue;
+                    bv[v] = fma(Jr[v], e[r], bv[v]);
+#pragma unroll
+                    for (int c = 0; c <= v; ++c)
+                        if ((P.tgt_mask >> c) & 1u) A[v][c] = fma(Jr[v], Jr[c], A[v][c]);
+                }
+            }
+        }
+        if constexpr (S > 1) {  // gather the owned rows into every lane of the group (structural zeros stay 0)
 #pragma unroll
             for (int v = 0; v < MAXV; ++v) {
-                if (!((P.tgt_mask >> v) & 1u)) continue;
-                bv[v] = fma(Jr[v], e[r], bv[v]);
+                const int o = v / S, ow = v % S;
+                auto bc = [&](T x) { return S == 16 ? row_bcast16(x, ow) : lane_bcast(x, gbase + ow); };
+                const uint32_t nz = P.nzrow[v];
+                bv[v] = ((nz >> v) & 1u) ? bc(bo[o]) : T(0);
 #pragma unroll
-                for (int c = 0; c <= v; ++c)
-                    if ((P.tgt_mask >> c) & 1u) A[v][c] = fma(Jr[v], Jr[c], A[v][c]);
+                for (int c = 0; c <= v; ++c) A[v][c] = ((nz >> c) & 1u) ? bc(Ao[o][c]) : T(0);
             }
         }
         KIN_IKT_STAMP(5);

@@ -172,6 +172,9 @@ struct KIkcProg {
     int32_t pad;
     T Xt[12];           // target link frame = frame(tgt_step) * Xt
     T vlo[kIkcMaxVars], vhi[kIkcMaxVars];  // joint limits of the variables (base: +-inf)
+    // structure of the normal equations: bit c of nzrow[v] (c <= v) is set when entry (v, c) can be nonzero --
+    // v and c both move the target link or both move one sphere (every other entry is exactly 0)
+    uint32_t nzrow[kIkcMaxVars];
 };
 
 // kernel-side tiling: workgroup b works on tile b / tile_blocks (0xffffffff: plain SoA)
