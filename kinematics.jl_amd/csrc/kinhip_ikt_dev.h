@@ -87,6 +87,19 @@ __device__ __forceinline__ T pick_lane(const T (&a)[N], int i) {
     }
     return t[0];
 }
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+// a[O + i] for a per-lane i in [0, S) (a lane's row of the O-th round of S rows; O + i >= N gives a[N - 1])
+template <int O, int S, typename T, int N>
+__device__ __forceinline__ T pick_round(const T (&a)[N], int i) {
+    constexpr int M = N - O < S ? N - O : S;  // rows of this round that exist
+    T sub[M > 0 ? M : 1];
+#pragma unroll
+    for (int k = 0; k < (M > 0 ? M : 1); ++k) sub[k] = a[M > 0 ? O + k : N - 1];
+    return pick_lane(sub, i);
+}
 template <typename T, int N>
 __device__ __forceinline__ void put(T (&a)[N], int i, T v) {
 #pragma unroll
@@ -496,17 +509,20 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                             for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? bc(av[rr][v]) : T(0);
                         }
                     // this lane's rows (accum_row's operations on them)
-#pragma unroll
-                    for (int o = 0; o < NRO; ++o) {
+                    auto own = [&](auto oc) {
+                        constexpr int o = decltype(oc)::value;
                         const int v = o * S + sl;
                         if (v < MAXV && ((anc >> v) & 1u)) {  // (per lane)
-                            const T wr = w2 * pick_lane(ak, v);
+                            const T wr = w2 * pick_round<o * S, S>(ak, sl);
                             bo[o] = fma(wr, vk, bo[o]);
 #pragma unroll
                             for (int c = 0; c < MAXV; ++c)
                                 if ((anc >> c) & 1u) Ao[o][c] = fma(wr, ak[c], Ao[o][c]);
                         }
-                    }
+                    };
+                    own(IntC<0>());
+                    if constexpr (NRO > 1) own(IntC<1>());
+                    static_assert(NRO <= 2, "rows per lane (MAXV <= 2 S)");
                 }
             }
         }
@@ -597,17 +613,19 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 else Jr[v] = r == 3 ? x : r == 4 ? y : z;
             }
             if constexpr (S > 1) {  // the owned rows
-#pragma unroll
-                for (int o = 0; o < NRO; ++o) {
+                auto own = [&](auto oc) {
+                    constexpr int o = decltype(oc)::value;
                     const int v = o * S + sl;
                     if (v < MAXV && ((P.tgt_mask >> v) & 1u)) {  // (per lane)
-                        const T jv = pick_lane(Jr, v);
+                        const T jv = pick_round<o * S, S>(Jr, sl);
                         bo[o] = fma(jv, e[r], bo[o]);
 #pragma unroll
                         for (int c = 0; c < MAXV; ++c)
                             if ((P.tgt_mask >> c) & 1u) Ao[o][c] = fma(jv, Jr[c], Ao[o][c]);
                     }
-                }
+                };
+                own(IntC<0>());
+                if constexpr (NRO > 1) own(IntC<1>());
             } else {
 #pragma unroll
                 for (int v = 0; v < MAXV; ++v) {
