@@ -69,13 +69,18 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
         // most 2 moving groups (24 fewer registers for the per-lane group frames than the 4-group one)
         const hipFunction_t jk = jf ? jf->coll_scene[grads ? 1 : 0][sl.ng <= 2 ? 0 : 1] : nullptr;
         if (jk) {
+            // the 2-group kernel keeps its lanes' group frames in LDS after the boxes (coll_body, SceneCtx)
+            static const bool frames_lds = ab_env_int("KINHIP_SCENE_LDS", 0) != 0;  // (A/B build; see kinhip_jit.cpp)
+            const size_t ldsj = sl.ng <= 2 && frames_lds && scene_frames_in_lds<T>(2)
+                                    ? (lds + 15) / 16 * 16 + 2 * 12 * 256 * sizeof(T)
+                                    : lds;
             int64_t cc = c;
             CollArgs ac = a;
             Tiling tc = tl;
             void* args[] = {(void*)&boxes, (void*)&ac, (void*)&qc, (void*)&ldq, (void*)&cc, (void*)&dc, (void*)&ldd,
                             (void*)&gc, (void*)&ldg, (void*)&mc, (void*)&tc, (void*)&sa};
             const hipError_t e = hipModuleLaunchKernel(jk, grid.x, 1, 1, 256, 1, 1,
-                                                       (unsigned)coll_lds(lds), st, args, nullptr);
+                                                       (unsigned)coll_lds(ldsj), st, args, nullptr);
             if (e != hipSuccess) return e;
             continue;
         }

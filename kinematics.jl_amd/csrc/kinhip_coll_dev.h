@@ -192,12 +192,36 @@ struct SceneArgs {
     int32_t base_col = -1;   // scene planar base (x, y, theta) columns, -1: none
     int32_t uniform = 0;     // 1: every sample uses the scene column values of sample 0
 };
-template <typename T, int MAXG>
+// The group frames of a lane: in registers (12 per group), or with LF in LDS slots of the lane
+// (element (g, j) at lf[(g * 12 + j) * B]: consecutive lanes, no bank conflicts) -- the specialised fp32
+// door-sweep kernel, whose 2 x 12 frame registers are what keeps it at 4 waves per SIMD (KINHIP_SCENE_LDS)
+template <typename T, int MAXG, bool LF = false>
 struct SceneCtx {
     KSceneGroup gr[MAXG];  // the groups' descriptors, loaded once (uniform: scalar registers)
     int ng;
-    T inv[MAXG][12];  // per lane: world -> group frame (row-major 3x4); MAXG >= ng (register budget)
+    T inv[LF ? 1 : MAXG][12];  // per lane: world -> group frame (row-major 3x4); MAXG >= ng (register budget)
+    __attribute__((address_space(3))) T* lf = nullptr;
+    int B = 0;
+    __device__ __forceinline__ T at(int g, int j) const {
+        if constexpr (LF) return lf[(g * 12 + j) * B];
+        else return inv[g][j];
+    }
+    __device__ __forceinline__ void set(int g, int j, T v) {
+        if constexpr (LF) lf[(g * 12 + j) * B] = v;
+        else inv[g][j] = v;
+    }
 };
+// (measured and not kept: the frames in LDS, 115 -> 103 VGPRs, still 4 waves per SIMD, door sweep 130 -> 143 us;
+// with 5 waves forced, 7 VGPR spills, 144 us -- profiles/r05_scene_lds_ab.txt.  A/B build: KINHIP_SCENE_LDS=1)
+#ifndef KINHIP_SCENE_LDS
+#define KINHIP_SCENE_LDS 0
+#endif
+// whether a scene kernel of `scene_groups` groups keeps the lane frames in LDS, after the boxes (kinhip_coll.hip
+// sizes the launch: 12 * scene_groups * blockDim values)
+template <typename T>
+__host__ __device__ constexpr bool scene_frames_in_lds(int scene_groups) {
+    return KINHIP_SCENE_LDS && sizeof(T) == 4 && scene_groups > 0 && scene_groups <= 2;
+}
 
 // rotation by th about the unit axis u (Rodrigues; the reference's UnitQuaternion(cos th/2, u sin th/2))
 template <typename T>
@@ -211,8 +235,8 @@ __device__ __forceinline__ void axis_rotation(const T* __restrict__ u, T th, T (
 }
 
 // the group frames of this sample (get_transform(scene, link) up to the group's moving frame), inverted
-template <typename T, int MAXG>
-__device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG>& sc, const SceneArgs<T>& sa, uint32_t off) {
+template <typename T, int MAXG, bool LF>
+__device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG, LF>& sc, const SceneArgs<T>& sa, uint32_t off) {
     sc.ng = sa.ng;
     const uint32_t so = sa.uniform ? 0u : off;
 #pragma unroll
@@ -251,16 +275,16 @@ __device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG>& sc, const SceneA
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j) sc.inv[g][4 * i + j] = f.r[3 * j + i];
-            sc.inv[g][4 * i + 3] = -fma(f.r[i], f.t[0], fma(f.r[3 + i], f.t[1], f.r[6 + i] * f.t[2]));
+            for (int j = 0; j < 3; ++j) sc.set(g, 4 * i + j, f.r[3 * j + i]);
+            sc.set(g, 4 * i + 3, -fma(f.r[i], f.t[0], fma(f.r[3 + i], f.t[1], f.r[6 + i] * f.t[2])));
         }
     }
 }
 
 // UnionSDF over the scene's groups: each group's boxes in its own frame (union_sdf), the first minimum
 // over groups; the gradient rotated back to the world
-template <typename T, bool GRAD, int NS, int MAXG>
-__device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const KBox<T>* __restrict__ boxes,
+template <typename T, bool GRAD, int NS, int MAXG, bool LF>
+__device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG, LF>& sc, const KBox<T>* __restrict__ boxes,
                                             const KAabb<T>* __restrict__ aabb, const T (&px)[NS], const T (&py)[NS],
                                             const T (&pz)[NS], T (&d)[NS], T (&gw)[NS][3], const unsigned char* smem,
                                             bool use_lds) {
@@ -276,7 +300,9 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const K
     for (int g = 0; g < MAXG; ++g) {
         if (g >= sc.ng) break;  // uniform
         const KSceneGroup& G = sc.gr[g];
-        const T* I = sc.inv[g];
+        T I[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) I[j] = sc.at(g, j);
         T lx[NS], ly[NS], lz[NS];
         // Exact cull: every box of the group lies in its enclosing box (bc, bh), so the distance to that
         // box is a lower bound of the group's distance; a group that cannot come below the minimum of the
@@ -321,13 +347,18 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG>& sc, const K
         for (int i = 0; i < NS; ++i) {
             if (wg[i] < 0) continue;  // no group below +inf (NaN input): a zero gradient
             T I[12];
+            if constexpr (LF) {  // the winning group's frame: one LDS read per entry at the lane's own index
 #pragma unroll
-            for (int j = 0; j < 12; ++j) I[j] = sc.inv[0][j];
+                for (int j = 0; j < 12; ++j) I[j] = sc.at(wg[i], j);
+            } else {
 #pragma unroll
-            for (int g = 1; g < MAXG; ++g) {
-                if (g >= sc.ng) break;  // uniform
+                for (int j = 0; j < 12; ++j) I[j] = sc.inv[0][j];
 #pragma unroll
-                for (int j = 0; j < 12; ++j) I[j] = wg[i] == g ? sc.inv[g][j] : I[j];
+                for (int g = 1; g < MAXG; ++g) {
+                    if (g >= sc.ng) break;  // uniform
+#pragma unroll
+                    for (int j = 0; j < 12; ++j) I[j] = wg[i] == g ? sc.inv[g][j] : I[j];
+                }
             }
             const T lx = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
             const T ly = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
@@ -369,7 +400,7 @@ __device__ __forceinline__ void coll_spheres(int s_last, int k0, int k1, const F
                                              uint32_t off, T* __restrict__ dists, int64_t ldd,
                                              T* __restrict__ grads, int64_t ldg, T& dmin,
                                              const unsigned char* smem, bool use_lds,
-                                             const SceneCtx<T, SCENE ? SCENE : 1>* sc = nullptr) {
+                                             const SceneCtx<T, SCENE ? SCENE : 1, scene_frames_in_lds<T>(SCENE)>* sc = nullptr) {
     const int ndof = P.n_jac + ((P.flags & PF_BASE) ? 3 : 0);
     // paired stores (KINHIP_COLL_STPAIR): every lane of the wave active, rows 8-byte aligned
     const bool pair_ok = GRAD && KINHIP_COLL_STPAIR && grads && (ldg & 1) == 0 &&
@@ -564,7 +595,14 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
     const T trunc = (T)a.truncation;
     const T offs = (T)a.offset;
     const bool broad = SCENE == 0 && isfinite(a.truncation);  // uniform (attached boxes: no union bound)
-    SceneCtx<T, SCENE ? SCENE : 1> sc;
+    constexpr bool LFS = scene_frames_in_lds<T>(SCENE);
+    SceneCtx<T, SCENE ? SCENE : 1, LFS> sc;
+    if constexpr (LFS) {  // this lane's frame slots after the boxes (the launcher sizes the LDS)
+        const int boff = use_lds ? (a.n_boxes * (int)sizeof(KBox<T>) + 15) / 16 * 16 : 0;
+        sc.lf = (__attribute__((address_space(3))) T*)((__attribute__((address_space(3))) unsigned char*)smem + boff) +
+                threadIdx.x;
+        sc.B = (int)blockDim.x;
+    }
     if constexpr (SCENE != 0) scene_frames(sc, sa, off);  // (plain SoA only: kin_coll_batch_scene)
     const T bnd[6] = {(T)a.bc[0], (T)a.bc[1], (T)a.bc[2], (T)a.bh[0], (T)a.bh[1], (T)a.bh[2]};
     T dmin = T(INFINITY);

@@ -221,14 +221,14 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             // hold never reaches a workgroup that has to wait for a slot.  Round 4 dealt the list over the
             // WHOLE grid (4,096 workgroups at config 4): the fp64 kernel, two resident workgroups per CU,
             // then ran a 1,000-wave list in two rounds of one busy wave per workgroup (config 4 fp64
-            // 0.145 -> 0.365 ms, BENCH_r04; A/B profiles/r05_ik_p2_ab.txt).  Measured (round 5): the spread
-            // over the resident workgroups helps the fp64 kernel (2 workgroups per CU; damped config 4 0.172 ->
-            // 0.158 ms) and costs the fp32 one (3 per CU: 0.073 -> 0.087 ms; co-resident workgroups stack their
-            // first waves), so it applies to kernels of at most 2 resident workgroups per CU; others and the
-            // generic kernels run block-major (round 3's order).  KINHIP_IK_P2_SPREAD=<0 never | 1 (default) |
+            // 0.145 -> 0.365 ms, BENCH_r04; A/B profiles/r05_ik_p2_ab.txt).  Measured (round 5,
+            // profiles/r05_ik_p2_ab2.txt): the spread over the resident workgroups costs the fp32 kernels
+            // (config 4 fixed lambda 0.071 -> 0.089 ms, damped 0.072 -> 0.084) and fp64 at fixed lambda (0.154
+            // -> 0.163), and helps only damped fp64 (0.171 -> 0.158): every kernel runs block-major (round 3's
+            // order).  KINHIP_IK_P2_SPREAD=<0 never (default) | 1 kernels of <= 2 resident workgroups per CU |
             // 2 always | 3 whole grid (round 4)>, KINHIP_IK_P2_BLOCK=<64|256> (A/B build).
             static const int p2_block_env = ab_env_int("KINHIP_IK_P2_BLOCK", 256);
-            static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 1);
+            static const int spread_env = ab_env_int("KINHIP_IK_P2_SPREAD", 0);
             const int bs2 = p2_block_env == 64 ? 64 : 256;
             a2.p2_spread = 0;
             if (spread_env != 0 && bs2 == 256 && jf) {  // (the resident workgroups of the phase-2 kernel)

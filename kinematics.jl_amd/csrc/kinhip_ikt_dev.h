@@ -282,6 +282,11 @@ __device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>
 // returns the best point it found.  NR: rounds of spheres per lane (ceil(n_sph / S); S > 1 only in
 // the specialised kernels, where the program is constant).  MAXG > 0: boxes attached to a scene,
 // one set of scene joint values per target (sa).
+// S > 1: the rows of the normal equations owned by the group's lanes (1) or formed by every lane (0; A/B:
+// KINHIP_JIT_DEFS=-DKINHIP_IKT_OWN=0) -- identical results
+#ifndef KINHIP_IKT_OWN
+#define KINHIP_IKT_OWN 1
+#endif
 template <typename T, int MAXV, int ROWS, int G, int S, int NR, int MAXG>
 __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>* __restrict__ St,
                                          const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
@@ -390,7 +395,8 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         // kernel (spheres in order, then the pose rows), so the results are bit-identical for every S; a group's
         // lanes no longer each form every entry (the sphere rows and the pose rows were ~2/3 of the FMAs of an
         // iteration, on the one-wave critical path of the batch's slowest target).
-        constexpr int NRO = S > 1 ? (MAXV + S - 1) / S : 1;
+        constexpr bool OWN = S > 1 && KINHIP_IKT_OWN;
+        constexpr int NRO = OWN ? (MAXV + S - 1) / S : 1;
         T Ao[NRO][MAXV], bo[NRO];
 #pragma unroll
         for (int o = 0; o < NRO; ++o) {
@@ -508,6 +514,10 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
 #pragma unroll
                             for (int v = 0; v < MAXV; ++v) ak[v] = ((anc >> v) & 1u) ? bc(av[rr][v]) : T(0);
                         }
+                    if constexpr (!OWN) {
+                        accum_row<T, MAXV>(A, bv, ak, vk, w2, anc);
+                        continue;
+                    }
                     // this lane's rows (accum_row's operations on them)
                     auto own = [&](auto oc) {
                         constexpr int o = decltype(oc)::value;
@@ -612,7 +622,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                                                                             : fma(kr[4], x, fma(kr[5], y, z));
                 else Jr[v] = r == 3 ? x : r == 4 ? y : z;
             }
-            if constexpr (S > 1) {  // the owned rows
+            if constexpr (OWN) {  // the owned rows
                 auto own = [&](auto oc) {
                     constexpr int o = decltype(oc)::value;
                     const int v = o * S + sl;
@@ -637,7 +647,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 }
             }
         }
-        if constexpr (S > 1) {  // gather the owned rows into every lane of the group (structural zeros stay 0)
+        if constexpr (OWN) {  // gather the owned rows into every lane of the group (structural zeros stay 0)
 #pragma unroll
             for (int v = 0; v < MAXV; ++v) {
                 const int o = v / S, ow = v % S;

@@ -5,14 +5,15 @@ The product library libkinhip.so never reads these variables (kinhip_internal.h 
     python tools/ab.py <workload> [--reps R] [SETTING ...]
       workload: ik (tools/ik_ab.py: config-4 IK), coll (tools/coll_spec_ab.py: config-5 k_coll legs),
                 fk (tools/fk_legs_ab.py: headline FK + J and config 2), jl (tools/jl_layout_ab.py: FK + J at
-                ld = N, the Julia shim's layout)
+                ld = N, the Julia shim's layout), scene (tools/scene_ab.py: the f2 door sweep), cik (tools/cik_ab.py:
+                the f2 / f3 legs, stage-2 times)
       SETTING:  "NAME=VALUE[,NAME=VALUE...]" -- one run per setting; "base" = no knob
     e.g. python tools/ab.py ik base KINHIP_IK_TWO_PHASE=0 KINHIP_IK_GROUP=2,KINHIP_IK_TWO_PHASE=0
          python tools/ab.py coll base "KINHIP_JIT_DEFS=-DKINHIP_AABB_UNROLL=1" KINHIP_COLL_FAST_TRIG=0
 
 Knobs (all read only by the A/B build): KINHIP_IK_GROUP, KINHIP_IK_RESIDENT, KINHIP_IK_QUEUE,
 KINHIP_IK_TWO_PHASE, KINHIP_IK_TP_QUEUE (IK schedule), KINHIP_IKC_GROUP (collision-aware IK lanes), KINHIP_FK_PER_LANE (FK grid), KINHIP_JIT_IK_WAVES,
-KINHIP_JIT_COLL_WAVES (occupancy), KINHIP_COLL_FAST_TRIG, KINHIP_IK_FAST_ATAN (arithmetic variants),
+KINHIP_JIT_COLL_WAVES (occupancy), KINHIP_COLL_FAST_TRIG, KINHIP_IK_FAST_ATAN (arithmetic variants), KINHIP_SCENE_LDS (scene frames in LDS),
 KINHIP_JIT_SLP, KINHIP_JIT_DEFS, KINHIP_JIT_OPTS (compiler options / definitions), KINHIP_JIT_DUMP
 (keep the generated source).  Every run prints its workload's own result line prefixed by the setting."""
 import os
@@ -20,7 +21,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SCRIPTS = {"ik": "ik_ab.py", "coll": "coll_spec_ab.py", "fk": "fk_legs_ab.py", "jl": "jl_layout_ab.py"}
+SCRIPTS = {"ik": "ik_ab.py", "coll": "coll_spec_ab.py", "fk": "fk_legs_ab.py", "jl": "jl_layout_ab.py",
+           "scene": "scene_ab.py", "cik": "cik_ab.py"}
 
 
 def main(argv):

@@ -17,7 +17,8 @@
 #                               tools/prof_kernel.py (e.g. fkjac32ts, ik32s, coll32s, collg32s, cik32s)
 #   ik                          config-4 IK timing (product, twice) and 1M targets; per-iteration probe
 #   ik-sections                 iteration section stamps (A/B build, -DKINHIP_IK_SECT=k)
-#   ikt-sections                collision-aware IK (f3 stage 2) section stamps (A/B build, -DKINHIP_IKT_SECT=k)
+#   ikt-sections[=<defs>]       collision-aware IK (f3 stage 2) section stamps (A/B build, -DKINHIP_IKT_SECT=k
+#                               plus the given definitions, e.g. ikt-sections=-DKINHIP_IKT_OWN=0)
 #   ik-timeline                 per-lane entry / write timeline of one solve (A/B build)
 #   ik-dump                     the specialised IK source (A/B build, KINHIP_JIT_DUMP) + a kernel trace of config 4
 #   coll                        the plain-row padding A/B of the config-5 legs (tools/coll_pad_ab.py)
@@ -100,9 +101,10 @@ for step in "$@"; do
       for k in 1 2 3 4 5 6 7; do
         timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=$k python -u tools/ik_sect.py 2>&1 | quiet || exit 8
       done ;;
-    ikt-sections)
+    ikt-sections|ikt-sections=*)
+      xd=${step#ikt-sections}; xd=${xd#=}
       for k in 1 2 3 4 5 6 7; do
-        timeout -k 10 180 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IKT_SECT=$k python -u tools/ikt_sect.py 2>&1 | quiet || exit 8
+        timeout -k 10 180 env KINHIP_LIB=$AB "KINHIP_JIT_DEFS=-DKINHIP_IKT_SECT=$k $xd" python -u tools/ikt_sect.py 2>&1 | quiet || exit 8
       done ;;
     ik-timeline)
       timeout -k 10 120 env KINHIP_LIB=$AB KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=9 python -u tools/ik_timeline.py 2>&1 | quiet || exit 8 ;;

@@ -9,7 +9,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "kinematics.jl_amd", "csrc")
+CSRC = os.environ.get("KINHIP_CSRC", os.path.join(ROOT, "kinematics.jl_amd", "csrc"))  # (another tree: A/B)
 HDRS = ["kinhip_prog.h", "kinhip_device.h", "kinhip_fk_dev.h", "kinhip_ik_dev.h", "kinhip_coll_dev.h", "kinhip_ikt_dev.h"]
 OPTS = ["-ffp-contract=fast-honor-pragmas", "-DKINHIP_COLL_SOFF=1", "-DKINHIP_COLL_FAST_TRIG=1",
         "-DKINHIP_IK_FAST_ATAN=1"]
@@ -51,7 +51,8 @@ def main(argv):
     if not os.path.exists(tool):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O2", os.path.join(ROOT, "tools", "jit_rtc_check.cpp"), "-o", tool,
                         "-lhiprtc"], check=True)
-    r = subprocess.run([tool, path, argv[2]] + OPTS, capture_output=True, text=True)
+    extra = os.environ.get("KINHIP_OFFLINE_DEFS", "").split()  # (e.g. -DKINHIP_IKT_SECT=5)
+    r = subprocess.run([tool, path, argv[2]] + OPTS + extra, capture_output=True, text=True)
     sys.stderr.write(r.stderr[-4000:])
     return r.returncode
 
