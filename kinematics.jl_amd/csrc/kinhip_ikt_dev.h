@@ -144,18 +144,60 @@ __device__ __forceinline__ void sphere_row(const KIkcProg<T>& P, uint32_t anc, T
 }
 
 // w^2 a a^T and w^2 viol a into the lower triangle of the normal equations, over the variables of anc
+// A[r][c] = fma(w[r], x[c], A[r][c]) for every r, c <= r of `mask` (the lower triangle's entries that row r
+// and column c both reach; others untouched).  fp32 with KINHIP_IKT_PK: entries (r, c) and (r, c + 1) of one
+// row as one v_pk_fma_f32 with w[r] broadcast where both are in the mask -- each element the same fma, so the
+// results are identical (one wave per SIMD issues a packed FMA in ~1.5x the time of a scalar one,
+// tools/pk_probe.hip: the pair costs 0.75 of its scalar FMAs)
+#ifndef KINHIP_IKT_PK
+#define KINHIP_IKT_PK 1
+#endif
+template <typename T, int MAXV>
+__device__ __forceinline__ void lower_rank1(T (&A)[MAXV][MAXV], const T (&w)[MAXV], const T (&x)[MAXV], uint32_t mask) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    // (the pairs only where the mask is a constant -- the specialised kernels; the generic ones keep the
+    // scalar loop rather than a run-time test per pair)
+    if (!__builtin_constant_p(mask)) {
+#pragma unroll
+        for (int r = 0; r < MAXV; ++r) {
+            if (!((mask >> r) & 1u)) continue;
+#pragma unroll
+            for (int c = 0; c <= r; ++c)
+                if ((mask >> c) & 1u) A[r][c] = fma(w[r], x[c], A[r][c]);
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < MAXV; ++r) {
+        if (!((mask >> r) & 1u)) continue;
+#pragma unroll
+        for (int c = 0; c <= r; ++c) {
+            if (!((mask >> c) & 1u)) continue;
+            if constexpr (KINHIP_IKT_PK && sizeof(T) == 4) {
+                if (c + 1 <= r && ((mask >> (c + 1)) & 1u) && (c & 1) == 0) {
+                    const f2 v = __builtin_elementwise_fma(f2{(float)w[r], (float)w[r]}, f2{(float)x[c], (float)x[c + 1]},
+                                                           f2{(float)A[r][c], (float)A[r][c + 1]});
+                    A[r][c] = (T)v.x;
+                    A[r][c + 1] = (T)v.y;
+                    continue;
+                }
+                if (c >= 1 && (c & 1) == 1 && ((mask >> (c - 1)) & 1u)) continue;  // (done with its pair)
+            }
+            A[r][c] = fma(w[r], x[c], A[r][c]);
+        }
+    }
+}
+
 template <typename T, int MAXV>
 __device__ __forceinline__ void accum_row(T (&A)[MAXV][MAXV], T (&bv)[MAXV], const T (&av)[MAXV], T viol, T w2,
                                           uint32_t anc) {
+    T wr[MAXV];
 #pragma unroll
     for (int r = 0; r < MAXV; ++r) {
-        if (!((anc >> r) & 1u)) continue;
-        const T wr = w2 * av[r];
-        bv[r] = fma(wr, viol, bv[r]);
-#pragma unroll
-        for (int c = 0; c <= r; ++c)
-            if ((anc >> c) & 1u) A[r][c] = fma(wr, av[c], A[r][c]);
+        wr[r] = w2 * av[r];
+        if ((anc >> r) & 1u) bv[r] = fma(wr[r], viol, bv[r]);
     }
+    lower_rank1<T, MAXV>(A, wr, av, anc);
 }
 
 // min over the S lanes of an aligned group (S <= 16, inside one DPP row): quad_perm [1,0,3,2], [2,3,0,1],
@@ -282,10 +324,12 @@ __device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>
 // returns the best point it found.  NR: rounds of spheres per lane (ceil(n_sph / S); S > 1 only in
 // the specialised kernels, where the program is constant).  MAXG > 0: boxes attached to a scene,
 // one set of scene joint values per target (sa).
-// S > 1: the rows of the normal equations owned by the group's lanes (1) or formed by every lane (0; A/B:
-// KINHIP_JIT_DEFS=-DKINHIP_IKT_OWN=0) -- identical results
+// S > 1: the rows of the normal equations formed by every lane of the group (0) or owned by the group's lanes
+// and gathered (1; A/B: KINHIP_JIT_DEFS=-DKINHIP_IKT_OWN=1) -- identical results.  Ownership cuts the loop's
+// FMAs 1,140 -> 658 (offline ISA) and yet measured slower on every leg (stage 2 of f3 0.152 -> 0.231 ms, the
+// scene door 0.198 -> 0.349, PR2 0.67 -> 2.29; profiles/r05_ikt_own_ab.txt): not kept
 #ifndef KINHIP_IKT_OWN
-#define KINHIP_IKT_OWN 1
+#define KINHIP_IKT_OWN 0
 #endif
 template <typename T, int MAXV, int ROWS, int G, int S, int NR, int MAXG>
 __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>* __restrict__ St,
@@ -481,11 +525,22 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             T av[NR][MAXV], viol[NR];
             uint64_t inband[NR];
             T dl = T(INFINITY);
+            // every round's sphere of this lane in one pass over the union (its boxes loaded once; each
+            // point's arithmetic is the one-point pass's)
+            T xs[NR], ys[NR], zs[NR], ds[NR], gs[NR][3];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                xs[r] = pc[r][0];
+                ys[r] = pc[r][1];
+                zs[r] = pc[r][2];
+            }
+            if constexpr (MAXG > 0) scene_union<T, true, NR, MG>(sc, boxes, aabb, xs, ys, zs, ds, gs, smem, use_lds);
+            else union_sdf<T, true, NR>(boxes, aabb, ca.n_aabb, ca.n_boxes, xs, ys, zs, ds, gs, smem, use_lds);
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const bool valid = r * S + sl < P.n_sph;
-                T dr, g[3];
-                sdf_at(pc[r][0], pc[r][1], pc[r][2], dr, g);
+                const T dr = ds[r];
+                const T g[3] = {gs[r][0], gs[r][1], gs[r][2]};
                 const T d = dr - prad[r];
                 dl = valid ? fmin(dl, d) : dl;
                 viol[r] = act - d;
@@ -638,13 +693,9 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 if constexpr (NRO > 1) own(IntC<1>());
             } else {
 #pragma unroll
-                for (int v = 0; v < MAXV; ++v) {
-                    if (!((P.tgt_mask >> v) & 1u)) continue;
-                    bv[v] = fma(Jr[v], e[r], bv[v]);
-#pragma unroll
-                    for (int c = 0; c <= v; ++c)
-                        if ((P.tgt_mask >> c) & 1u) A[v][c] = fma(Jr[v], Jr[c], A[v][c]);
-                }
+                for (int v = 0; v < MAXV; ++v)
+                    if ((P.tgt_mask >> v) & 1u) bv[v] = fma(Jr[v], e[r], bv[v]);
+                lower_rank1<T, MAXV>(A, Jr, Jr, P.tgt_mask);
             }
         }
         if constexpr (OWN) {  // gather the owned rows into every lane of the group (structural zeros stay 0)
@@ -660,18 +711,24 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         }
         KIN_IKT_STAMP(5);
         // ---- the step --------------------------------------------------------------------------------
-        const uint32_t freev = active & ~held;
-#pragma unroll
-        for (int v = 0; v < MAXV; ++v) {
-            const bool fv = (freev >> v) & 1u;
-#pragma unroll
-            for (int c = 0; c < v; ++c)
-                if (!fv || !((freev >> c) & 1u)) A[v][c] = T(0);
-            A[v][v] = fv ? A[v][v] + a.lam2 : T(1);
-        }
+        // the variables held out of the step leave the system (rows and columns 0, diagonal 1).  While no lane of
+        // the wave holds one (the common case) the free set is the plan's `active` mask, a constant of the
+        // specialised kernels, and the masking folds away; the same operations either way
         T y[MAXV];
+        auto restrict_to = [&](uint32_t freev) {
 #pragma unroll
-        for (int v = 0; v < MAXV; ++v) y[v] = ((freev >> v) & 1u) ? bv[v] : T(0);
+            for (int v = 0; v < MAXV; ++v) {
+                const bool fv = (freev >> v) & 1u;
+#pragma unroll
+                for (int c = 0; c < v; ++c)
+                    if (!fv || !((freev >> c) & 1u)) A[v][c] = T(0);
+                A[v][v] = fv ? A[v][v] + a.lam2 : T(1);
+            }
+#pragma unroll
+            for (int v = 0; v < MAXV; ++v) y[v] = ((freev >> v) & 1u) ? bv[v] : T(0);
+        };
+        if (__builtin_constant_p(active) && __ballot(held != 0u) == 0) restrict_to(active);
+        else restrict_to(active & ~held);  // (the generic kernels: one copy of the run-time masking)
         // Cholesky (in place, lower) and the two triangular solves.  fp32: the reciprocal square root of
         // each pivot (v_rsq_f32) multiplies instead of the IEEE square root and divisions (~10 instructions
         // each, on the one-wave critical path); fp64 keeps the oracle's exact form (iterates to 1e-7)
@@ -724,8 +781,10 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             if ((P.joint_mask >> v) & 1u) {
                 const bool was = (held >> v) & 1u;
                 const T dir = was ? bv[v] : y[v];  // held: the descent direction J^T e + ...
-                if ((qs[v] <= P.vlo[v] && dir < T(0)) || (qs[v] >= P.vhi[v] && dir > T(0))) nh |= 1u << v;
-                if (was) y[v] = T(0);
+                // (bitwise, not short-circuit: selects instead of ~20 exec-mask instructions per joint)
+                const bool out = ((qs[v] <= P.vlo[v]) & (dir < T(0))) | ((qs[v] >= P.vhi[v]) & (dir > T(0)));
+                nh |= (uint32_t)out << v;
+                y[v] = was ? T(0) : y[v];
             }
             mx = fmax(mx, fabs(y[v]));
         }

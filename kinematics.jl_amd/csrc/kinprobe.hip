@@ -144,7 +144,7 @@ int launch_pattern(int64_t n, int64_t tile, int64_t ld, const float* q, float* o
 }  // namespace kinhip
 
 // rows_in / rows_out: (8, 60) FK + 6x8 J + pose (k_fk), (8, 126) 14 sphere distances + gradients
-// (k_coll, soffset-addressed outputs).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
+// (k_coll, soffset-addressed outputs), (12, 126) the same with 4 scene columns in (k_coll_scene).  Plain rows (tile = 0) ld >= n elements apart; tiled: ld = tile.
 // per_lane > 1: the grid-strided form with that many units per workgroup; -1: the LDS-staged 16-byte row stores
 // (p_pattern_x4, a layout experiment for k_fk).  lds: dynamic LDS bytes per
 // workgroup (0..65536) to cap the waves in flight per CU; blk: lanes per workgroup (64..256, a power of 2).
@@ -160,6 +160,8 @@ extern "C" __attribute__((visibility("default"))) int kinprobe_pattern4(int rows
         return kinhip::launch_pattern<8, 60, false>(n, tile, ld, q, out, per_lane, lds, blk, st);
     if (rows_in == 8 && rows_out == 126)
         return kinhip::launch_pattern<8, 126, true>(n, tile, ld, q, out, per_lane, lds, blk, st);
+    if (rows_in == 12 && rows_out == 126)  // (the f2 door sweep: q + the scene columns in)
+        return kinhip::launch_pattern<12, 126, true>(n, tile, ld, q, out, per_lane, lds, blk, st);
     return -2;
 }
 

@@ -208,14 +208,22 @@ def _run_scene(self, sdf, Q, dists, grads, min_dist, truncation, stream, scene_q
             raise ValueError(f"scene_q must be ({sdf.n_scene_cols}, N) with unit sample stride")
         lds = scene_q.stride(0)
     dev = Q.device
-    D = torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None
-    G = torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None
+    # (preallocated, row-padded output views as in run)
+    D = dists if isinstance(dists, torch.Tensor) else (
+        torch.empty((self.n_sph, N), dtype=self.dtype, device=dev) if dists else None)
+    G = grads if isinstance(grads, torch.Tensor) else (
+        torch.empty((self.n_sph, self.n_dof, N), dtype=self.dtype, device=dev) if grads else None)
     Mn = torch.empty(N, dtype=self.dtype, device=dev) if min_dist else None
+    for t, what in ((D, "dists"), (G, "grads")):
+        if t is not None:
+            _same_device(t, Q, what)
+    ldd = _ld_of(D.unsqueeze(0), (1, self.n_sph, N), self.dtype) if D is not None else N
+    ldg = _ld_of(G, (self.n_sph, self.n_dof, N), self.dtype) if G is not None else N
     st = (stream or torch.cuda.current_stream(dev)).cuda_stream
     ptr = lambda t: t.data_ptr() if t is not None else None
     K.check(K.lib().kin_coll_batch_scene(self._h, sdf._h, float(truncation), Q.data_ptr(), Q.stride(0),
-                                         scene_q.data_ptr() if scene_q.numel() else None, lds, N, ptr(D), N, ptr(G),
-                                         N, ptr(Mn), st))
+                                         scene_q.data_ptr() if scene_q.numel() else None, lds, N, ptr(D), ldd, ptr(G),
+                                         ldg, ptr(Mn), st))
     return D, G, Mn
 
 

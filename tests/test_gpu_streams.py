@@ -5,6 +5,7 @@ batches (two-phase schedule) back to back on that handle, each into its own outp
 equal the single-threaded reference bit for bit.  The same with one explicit stream per thread, and with
 one thread on the per-thread handle, as controls."""
 import ctypes as C
+import os
 import threading
 
 import pytest
@@ -77,14 +78,14 @@ def _run(config4, n_threads, streams, reps=6, sync_in_thread=True):
     return bad
 
 
-def test_two_threads_on_the_per_thread_stream_handle(config4):
+def test_two_threads_on_the_per_thread_stream_handle(config4, reps=int(os.environ.get("STREAMS_REPS", "6"))):
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    controls = {"one thread, per-thread handle": _run(config4, 1, [HIP_STREAM_PER_THREAD]),
-                "two threads, own streams": _run(config4, 2, [s1.cuda_stream, s2.cuda_stream])}
-    got = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD])
+    controls = {"one thread, per-thread handle": _run(config4, 1, [HIP_STREAM_PER_THREAD], reps),
+                "two threads, own streams": _run(config4, 2, [s1.cuda_stream, s2.cuda_stream], reps)}
+    got = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps)
     # (diagnostic, not asserted: without the in-thread synchronize, whether the device-wide one after
     # the threads have ended covers their per-thread streams)
-    nosync = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], sync_in_thread=False)
+    nosync = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps, sync_in_thread=False)
     print("mismatching targets per call:", controls, "two threads, per-thread handle:", got,
           "the same without the in-thread synchronize:", nosync)
     for name, bad in controls.items():

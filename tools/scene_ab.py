@@ -27,19 +27,33 @@ SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
 SQ[1] = 1.2
 SQ = SQ.to(dt).to(dev).contiguous()
 blocks = int(sys.argv[1]) if len(sys.argv) > 1 else 15
-run = lambda: cp.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ)  # noqa: E731
-for _ in range(5):
-    r = run()
+if os.environ.get("SCENE_AB_FRESH") == "1":  # (round 4's form: contiguous rows, outputs allocated per call)
+    run = lambda: cp.run(asdf, Q, grads=True, min_dist=True, scene_q=SQ)  # noqa: E731
+else:  # the bench leg's form: rows padded to n + 256, preallocated outputs
+    ld = n + 256
+    Qb = torch.empty((8, ld), dtype=dt, device=dev)
+    Qb[:, :n] = Q
+    SQb = torch.empty((4, ld), dtype=dt, device=dev)
+    SQb[:, :n] = SQ
+    Dp = torch.zeros((cp.n_sph, ld), dtype=dt, device=dev)[:, :n]
+    Gp = torch.zeros((cp.n_sph, 8, ld), dtype=dt, device=dev)[:, :, :n]
+    run = lambda: cp.run(asdf, Qb[:, :n], dists=Dp, grads=Gp, min_dist=True, scene_q=SQb[:, :n])  # noqa: E731
+# SCENE_AB_STREAM=1: launches on a created stream (the bench's _timed_calls form) instead of the null stream
+st = torch.cuda.Stream() if os.environ.get("SCENE_AB_STREAM") == "1" else torch.cuda.current_stream()
+with torch.cuda.stream(st):
+    for _ in range(5):
+        r = run()
 torch.cuda.synchronize()
 ts = []
 for _ in range(blocks):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(20):
-        r = run()
-    e1.record()
+    with torch.cuda.stream(st):
+        e0.record(st)
+        for _ in range(20):
+            r = run()
+        e1.record(st)
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1) / 20 * 1e3)
 chk = (float(r[0].double().abs().sum()), float(r[1].double().abs().sum()), float(r[2].double().sum()))
-print(f"scene median {statistics.median(ts):6.1f}us min {min(ts):6.1f}us chk {chk[0]:.9e} {chk[1]:.9e} {chk[2]:.9e}",
-      flush=True)
+print(f"scene median {statistics.median(ts):6.1f}us min {min(ts):6.1f}us max {max(ts):6.1f}us first {ts[0]:6.1f}us "
+      f"chk {chk[0]:.9e} {chk[1]:.9e} {chk[2]:.9e}", flush=True)
