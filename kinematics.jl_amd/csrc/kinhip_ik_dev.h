@@ -40,7 +40,14 @@ namespace {
 #endif
 // Contraction only inside one expression (a * b + c): the specialised kernels (hiprtc) fold constants
 // into the instruction stream, and fusing across statements would then differ from the generic ones
+#ifndef KINHIP_CONTRACT_FAST
+#define KINHIP_CONTRACT_FAST 0  // A/B only (KINHIP_JIT_DEFS): fusion across statements, spec != generic
+#endif
+#if KINHIP_CONTRACT_FAST
+#pragma clang fp contract(fast)
+#else
 #pragma clang fp contract(on)
+#endif
 // Diagnostic section stamps (tools only: KINHIP_JIT_DEFS=-DKINHIP_IK_SECT=<k> in the A/B build): the
 // cycles of iteration section k (1 FK, 2 errors + checks, 3 Jacobian + J W J^T, 4 Cholesky + solves,
 // 5 dq + active set, 6 step, 7 loop top) summed over the lane's iterations replace err row 0 and the

@@ -15,7 +15,14 @@
 
 // Contraction only inside one expression (a * b + c): the specialised kernels fold constants into the
 // instruction stream, and fusing across statements would then differ from the generic kernels
+#ifndef KINHIP_CONTRACT_FAST
+#define KINHIP_CONTRACT_FAST 0
+#endif
+#if KINHIP_CONTRACT_FAST
+#pragma clang fp contract(fast)
+#else
 #pragma clang fp contract(on)
+#endif
 
 // the specialised kernels unroll the tree walk and the sphere loops (constant trip counts)
 #ifdef KINHIP_JIT
