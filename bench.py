@@ -329,7 +329,10 @@ def _scene_and_coll_ik_legs(ctx, stream, n, steps, spec=1):
     SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
     SQ[1] = 1.2
     # plain SoA rows padded to ld = n + 256 and preallocated outputs, as config 5's distances + gradients leg
-    # (row-aligned 2^20-element streams share HBM channels; a fresh 450 MB output per call starts cold)
+    # (row-aligned 2^20-element streams share HBM channels; a fresh 450 MB output per call starts cold).
+    # Back-to-back launches of this kernel slow down in steps under sustained load (a rocprofv3 trace of the
+    # bench: 127 us for the first ~1 ms, then 138, 166, 177, settling near 155 us after ~5 ms; the box's power
+    # management -- profiles/r05_door_trace.txt); the leg keeps round 4's 3 warm-up launches + 20 timed ones
     pad = 256
     ld = n + pad
     Qb = torch.empty((8, ld), dtype=dt, device=ctx.device)
@@ -610,7 +613,7 @@ def _copy_bw(dev, nbytes=1 << 31):
 def _pmc_valu(fname):
     """Issue-based VALU busy of a committed PMC summary (tools/summarize_prof.py), for the legs whose
     bound is VALU / latency rather than HBM (configs 4 and 5)."""
-    for rnd in ("r04_", "r03_", "r02_"):  # the newest committed round's summary
+    for rnd in ("r05_", "r04_", "r03_", "r02_"):  # the newest committed round's summary
         p = os.path.join(ROOT, "profiles", rnd + fname)
         if os.path.exists(p):
             fname = rnd + fname

@@ -2029,8 +2029,15 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     if (!p->ik_busy[k] && p->ik_ev[k] && p->ik_stream[k] == stream &&
                         (!per_thread || p->ik_thread[k] == self))
                         set = k;
+                // A set whose last call ran on another thread's per-thread stream stays with that thread: its
+                // completion is known only through an event recorded on that thread's stream, and a round-5
+                // test saw two threads share a set on this handle -- so it is never
+                // handed across threads (at most kIkEagerSets such threads keep a set; later ones run one phase)
                 for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
-                    if (!p->ik_busy[k] && (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess)) set = k;
+                    if (!p->ik_busy[k] &&
+                        !(p->ik_ev[k] && p->ik_stream[k] == (void*)hipStreamPerThread && p->ik_thread[k] != self) &&
+                        (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess))
+                        set = k;
                 if (set >= 0) {
                     if (!p->ik_ev[set] && hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming) != hipSuccess) {
                         p->ik_ev[set] = nullptr;
