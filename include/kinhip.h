@@ -275,7 +275,9 @@ typedef struct kin_ik_params {
                            per plan: an eager call takes the set its stream used last, else a set whose
                            last call has finished on the device; when 4 calls of the plan are in flight on
                            other streams, the call runs the one-phase schedule (same results, slower)
-                           instead of sharing a set.  A captured graph keeps the set of its captured call. */
+                           instead of sharing a set.  On hipStreamPerThread "its stream" is per host thread,
+                           and a set last used there stays with that thread.  A captured graph keeps the set
+                           of its captured call. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */

@@ -75,3 +75,16 @@ def test_config4_answers_agree(setup, damp_err, max_step):
     assert same.mean() >= 0.98
     d = np.abs(Q.double().cpu().numpy() - rq).max(0)[same]
     assert np.percentile(d, 99) <= 5e-3, float(np.percentile(d, 99))
+    # the tail: EVERY target the fp32 kernel reports converged is a solution when its
+    # answer is checked in fp64 (the oracle's FK; position and axis-angle rotation error within the tolerance
+    # plus the fp32 FK / rotation-error rounding, 5e-6), whatever point of the solution set it ended on
+    conv = it <= 64
+    P = om.fk_batch(Q.double().cpu().numpy()[:, conv], ids, [gl.id])[0]
+    T = tgt[:, conv]
+    ep = np.linalg.norm(T[9:] - P[9:], axis=0)
+    Rt, Rq = T[:9].reshape(3, 3, -1), P[:9].reshape(3, 3, -1)  # [c][r][n]: element (r, c) at row r + 3 c
+    M = np.einsum("cin,cjn->ijn", Rt, Rq)  # Rt Rq^T (sum over the column index)
+    vee = 0.5 * np.stack([M[2, 1] - M[1, 2], M[0, 2] - M[2, 0], M[1, 0] - M[0, 1]])
+    er = np.arctan2(np.linalg.norm(vee, axis=0), 0.5 * (M[0, 0] + M[1, 1] + M[2, 2] - 1.0))
+    print(f"fp32 answers checked in fp64: max |dp| {ep.max():.3e}, max |drot| {er.max():.3e} over {int(conv.sum())}")
+    assert ep.max() <= 1e-3 + 5e-6 and er.max() <= 1e-3 + 5e-6, (float(ep.max()), float(er.max()))
