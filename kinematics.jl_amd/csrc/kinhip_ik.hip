@@ -195,6 +195,12 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             // full grid backfilled by the dispatcher is faster (profiles/r02_ik_queue_ab.txt)
             const int64_t plain1 = (c + 63) / 64;
             bool q1 = tpq_env != 0 && (qmode >= 0 ? qmode != 0 : plain1 > 2 * resident_waves);
+            // The fp32 kernels solve attempt 0's first KINHIP_IK_F64_ITERS iterations in fp64: on a queue a
+            // lane group that takes its next target runs those iterations while the rest of the wave is in
+            // fp32, so nearly every wave iteration pays both solves.  The plain grid starts a wave's targets
+            // together (1M targets: 0.607 -> 0.502 ms, identical results; profiles/r05_ik_1m_queue_ab.txt)
+            if (sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3 && KINHIP_IK_F64_ITERS > 0 && tpq_env < 0 && qmode < 0)
+                q1 = false;
             if (q1 && tpq_env < 0 && qmode < 0 && jf) {
                 const hipFunction_t f1 = jf->ik[a.with_rot ? 1 : 0][0];
                 int nb = 0;
