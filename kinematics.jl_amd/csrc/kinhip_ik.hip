@@ -72,9 +72,20 @@ static bool ik_two_phase(const IkArgs& a, int64_t n, int64_t c, int64_t cap) {
     return tp_env >= 0 ? tp_env != 0 : plain > ik_resident_waves();
 }
 
+// Launch chunk of a call: kIkChunk (32-bit lane offsets), and with restarts at most the two-phase scratch
+// capacity, so that a batch larger than one list still runs the two-phase schedule chunk by chunk (the chunks
+// run in stream order on the call's scratch set; each target's arithmetic is unchanged).  2M targets: 1.20 ms
+// on the one-phase queue before.
+static int64_t ik_chunk(const IkArgs& a, int64_t cap) {
+    int L, natt;
+    ik_attempts(a, &L, &natt);
+    return natt > 1 && a.lanes == 0 && cap > 0 ? std::min<int64_t>(kIkChunk, cap) : kIkChunk;
+}
+
 bool ik_wants_two_phase(const IkArgs& a, int64_t n, int64_t cap) {
-    for (int64_t s0 = 0; s0 < n; s0 += kIkChunk)
-        if (ik_two_phase(a, n, std::min<int64_t>(kIkChunk, n - s0), cap)) return true;
+    const int64_t chunk = ik_chunk(a, cap);
+    for (int64_t s0 = 0; s0 < n; s0 += chunk)
+        if (ik_two_phase(a, n, std::min<int64_t>(chunk, n - s0), cap)) return true;
     return false;
 }
 
@@ -157,7 +168,8 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
 #undef KIN_IK_G
         return hipGetLastError();
     };
-    const int64_t chunk = kIkChunk;  // lane byte offsets i * sizeof(T) stay below 2^32
+    // lane byte offsets i * sizeof(T) stay below 2^32; with a scratch set, chunks of at most its capacity
+    const int64_t chunk = scr.fail_list ? ik_chunk(a, scr.cap) : kIkChunk;
     for (int64_t s0 = 0; s0 < n; s0 += chunk) {
         at.ibase = a.index_base + s0;
         at.q0 = q0 ? q0 + s0 : nullptr;

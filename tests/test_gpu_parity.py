@@ -674,6 +674,26 @@ def test_ik_dls_two_phase_large_identical(dev, dtype):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
 
 
+def test_ik_dls_two_phase_chunked_identical(dev):
+    """A batch larger than the two-phase scratch list (2^20 + 5,000 targets) runs the two-phase schedule chunk
+    by chunk (ik_chunk: 2^20 and 5,000), phase 1 of the fp32 kernel on the plain grid; angles, iteration counts
+    and errors equal the one-phase schedule (lanes=4) bit for bit."""
+    m, arm = _fetch()
+    gl = m.find_link("gripper_link")
+    plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32)
+    plan.specialize()
+    N = (1 << 20) + 5000
+    Qt = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], N, seed=78,
+                                dtype=torch.float32, device=dev)
+    T = plan.run(Qt)[0][0].contiguous()
+    del Qt
+    kw = dict(max_iters=64, restarts=3, seed=5, lam=1e-2, max_step=0.5)
+    a = plan.ik_dls(T, torch.zeros((8, N), dtype=torch.float32, device=dev), lanes=0, **kw)
+    b = plan.ik_dls(T, torch.zeros((8, N), dtype=torch.float32, device=dev), lanes=4, **kw)
+    assert (a[1] > 16).any() and (a[1] <= 64).float().mean() > 0.99
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
 def test_ik_dls_work_queue_identical(dev, fetch_tree):
     """Large batches run as per-wave work queues (a lane group that finishes takes the wave's next
     target): bit-identical to one target per group (lanes=1 here never queues), and the first
