@@ -2032,7 +2032,10 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                 // A set whose last call ran on another thread's per-thread stream stays with that thread: its
                 // completion is known only through an event recorded on that thread's stream, and a round-5
                 // test saw two threads share a set on this handle -- so it is never
-                // handed across threads (at most kIkEagerSets such threads keep a set; later ones run one phase)
+                // handed across threads (at most kIkEagerSets such threads keep a set; later ones run one phase).
+                // (A thread that exits leaves its set reserved; a later thread that receives the same
+                // std::thread::id takes it over through the shortcut above, which is safe only if the exited
+                // thread's per-thread stream had drained -- HIP destroys that stream with the thread.)
                 for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
                     if (!p->ik_busy[k] &&
                         !(p->ik_ev[k] && p->ik_stream[k] == (void*)hipStreamPerThread && p->ik_thread[k] != self) &&
