@@ -2035,7 +2035,8 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                 // handed across threads (at most kIkEagerSets such threads keep a set; later ones run one phase).
                 // (A thread that exits leaves its set reserved; a later thread that receives the same
                 // std::thread::id takes it over through the shortcut above, which is safe only if the exited
-                // thread's per-thread stream had drained -- HIP destroys that stream with the thread.)
+                // thread's per-thread stream had drained; a caller synchronizes its per-thread stream before the
+                // thread ends, as tests/test_gpu_streams.py's workers do.)
                 for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
                     if (!p->ik_busy[k] &&
                         !(p->ik_ev[k] && p->ik_stream[k] == (void*)hipStreamPerThread && p->ik_thread[k] != self) &&
