@@ -272,12 +272,13 @@ typedef struct kin_ik_params {
                            round hands attempt 0 over after 5/8 of its iterations and phase 2 resumes it
                            beside the others, bit for bit).  The two-phase scratch (first call:
                            hipMalloc of 8 sets of ~16 MiB, 64 hand-over rings each, synchronising) is
-                           per plan: an eager call takes the set its stream used last, else a set whose
-                           last call has finished on the device; when 4 calls of the plan are in flight on
-                           other streams, the call runs the one-phase schedule (same results, slower)
-                           instead of sharing a set.  On hipStreamPerThread "its stream" is per host thread,
-                           and a set last used there stays with that thread.  A captured graph keeps the set
-                           of its captured call. */
+                           per plan: an eager call takes one of 4 sets and its stream waits on the device
+                           for the set's previous call (hipStreamWaitEvent) unless that call ran on the
+                           same stream, so calls from any thread, stream or handle (hipStreamPerThread
+                           included) never share a set in flight; the set its stream used last is
+                           preferred, else one that has finished, else the least recently used
+                           (kin_plan_ik_sched_stats counts the waits).  A captured graph keeps the set of
+                           its captured call. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */
@@ -310,6 +311,20 @@ KINHIP_API int kin_ik_dls_batch_from(const kin_plan* p, const kin_ik_params* prm
 KINHIP_API int kin_ik_dls_batch_trace(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt,
                                       const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* trace,
                                       int64_t ldtr, void* stream);
+
+/* Counters of the plan's two-phase IK scratch-set scheduling (kin_ik_params.lanes above), for tests and
+ * diagnostics; no reference counterpart (the reference is single-threaded). */
+typedef struct kin_ik_sched_stats {
+    uint64_t two_phase_calls;     /* eager calls that took a scratch set (two-phase schedule) */
+    uint64_t stream_waits;        /* of those, calls whose stream waited for another stream's call on the set */
+    uint64_t host_waits;          /* calls that found every set between take and event record in other
+                                     threads and waited (microseconds) for one */
+    uint64_t one_phase_fallbacks; /* eager two-phase calls that ran the one-phase schedule for want of a set
+                                     (0 by construction since ABI 2's hipStreamWaitEvent ordering) */
+    uint64_t captured_calls;      /* two-phase calls made inside a stream capture that took a graph set */
+    uint64_t captured_one_phase;  /* captured two-phase calls that ran one phase (the 4 graph sets taken) */
+} kin_ik_sched_stats;
+KINHIP_API int kin_plan_ik_sched_stats(const kin_plan* p, kin_ik_sched_stats* out);
 
 /* point_inverse_kinematics_nakamura (src/algorithm.jl:116-131), batched:
  * 50 SR-inverse iterations, `.+ sr_weight` broadcast quirk reproduced.

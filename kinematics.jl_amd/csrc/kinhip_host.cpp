@@ -19,7 +19,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <thread>
+#include <condition_variable>
 #include <sstream>
 #include <string>
 #include <type_traits>
@@ -210,25 +210,31 @@ struct kin_plan {
     JitKernels* jit = nullptr;
     uint32_t jit_mask = 0;
     // two-phase IK schedule scratch (launch_ik_dls): allocated by the first kin_ik_dls_batch call that
-    // runs the two-phase schedule.  An eager call takes an eager set (0..kIkEagerSets-1) that is safe
-    // for its stream: the set its stream used last (stream order serialises the two calls), else one
-    // whose last call has finished on the device (ik_ev) and that no other host thread is launching
-    // into (ik_busy); when every set is in flight on other streams the call runs the one-phase
-    // schedule (same results, no scratch) instead of sharing a list.  A call made inside a stream
-    // capture takes one of the remaining sets for good (the captured graph replays with it, so it
-    // never meets an eager call or another graph), and once those are gone further captures run the
-    // one-phase schedule.
+    // runs the two-phase schedule.  An eager call takes an eager set (0..kIkEagerSets-1) and is ordered
+    // after the set's previous call ON THE DEVICE: unless that call ran on the same stream (one handle
+    // other than hipStreamPerThread names one stream for every thread, so stream order serialises the
+    // two), the call's stream waits for the set's event (hipStreamWaitEvent) before its launches.  No
+    // host-side guess about which stream or thread a set belongs to is needed, so any thread, stream or
+    // handle may take any set.  The choice only affects concurrency: the set this stream used last,
+    // else one whose last call has finished, else the least recently used one (the wait then costs at
+    // most the overlap with that older call).  ik_busy covers the host window between taking a set and
+    // recording its event; a call that finds all sets in that window waits for one (ik_cv).  A call
+    // made inside a stream capture takes one of the remaining sets for good (the captured graph replays
+    // with it, so it never meets an eager call or another graph), and once those are gone further
+    // captures run the one-phase schedule.
     static constexpr int kIkScratchSets = 8;
     static constexpr int kIkEagerSets = 4;
     static constexpr int64_t kIkScratchCap = int64_t(1) << 20;
     mutable std::mutex ik_mu;
+    mutable std::condition_variable ik_cv;
     mutable void* d_ikscr = nullptr;
     mutable int ik_captured = 0;  // sets kIkEagerSets .. kIkEagerSets + ik_captured - 1 belong to graphs
-    mutable hipEvent_t ik_ev[kIkEagerSets] = {};      // recorded after a set's last call (null: unused)
-    mutable void* ik_stream[kIkEagerSets] = {};       // stream of that call
-    mutable std::thread::id ik_thread[kIkEagerSets];  // host thread of that call (per-thread stream handles)
-    mutable bool ik_busy[kIkEagerSets] = {};          // a host thread is launching into the set
-    mutable uint32_t ik_one_phase_fallbacks = 0;      // calls that found every set in flight (tests)
+    mutable hipEvent_t ik_ev[kIkEagerSets] = {};   // recorded after a set's last call (null: unused)
+    mutable void* ik_stream[kIkEagerSets] = {};    // stream handle of that call
+    mutable uint64_t ik_tick[kIkEagerSets] = {};   // when that call took the set (least recently used)
+    mutable bool ik_busy[kIkEagerSets] = {};       // a host thread is launching into the set
+    mutable uint64_t ik_ticks = 0;
+    mutable kin_ik_sched_stats ik_stats{};         // kin_plan_ik_sched_stats (tests)
     // collision-aware IK program (kin_coll_ik_plan_create, k_ik_tree): the needed tree, host copies
     // (plan specialisation) and one device allocation [KIkcStep<T> steps | KSphere<T> spheres]
     KIkcProg<float> ikf{};
@@ -2002,7 +2008,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         const bool capturing = cs == hipStreamCaptureStatusActive;
         int set = -1;
         {
-            std::lock_guard<std::mutex> lk(p->ik_mu);
+            std::unique_lock<std::mutex> lk(p->ik_mu);
             if (!p->d_ikscr) {
                 if (capturing)
                     return set_error(KIN_E_INVALID, "kin_ik_dls_batch: the plan's first two-phase call allocates its "
@@ -2018,42 +2024,49 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                 }
             }
             if (!capturing) {
-                // the set this stream used last, else a finished one, else none (one phase).  One handle
-                // names one stream for every host thread except hipStreamPerThread, which is each calling
-                // thread's own default stream: that handle matches only from the same thread.
-                // (The null stream is the device's legacy default stream, shared by every thread: this
-                // library is not built for per-thread default streams.)
+                // One handle names one stream for every host thread except hipStreamPerThread, which is
+                // each calling thread's own default stream: only a set last used through another handle
+                // than that one can be matched by handle.  (The null stream is the device's legacy default
+                // stream, shared by every thread: this library is not built for per-thread default streams.)
                 const bool per_thread = (hipStream_t)stream == hipStreamPerThread;
-                const std::thread::id self = std::this_thread::get_id();
-                for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
-                    if (!p->ik_busy[k] && p->ik_ev[k] && p->ik_stream[k] == stream &&
-                        (!per_thread || p->ik_thread[k] == self))
-                        set = k;
-                // A set whose last call ran on another thread's per-thread stream stays with that thread: its
-                // completion is known only through an event recorded on that thread's stream, and a round-5
-                // test saw two threads share a set on this handle -- so it is never
-                // handed across threads (at most kIkEagerSets such threads keep a set; later ones run one phase).
-                // (A thread that exits leaves its set reserved; a later thread that receives the same
-                // std::thread::id takes it over through the shortcut above, which is safe only if the exited
-                // thread's per-thread stream had drained; a caller synchronizes its per-thread stream before the
-                // thread ends, as tests/test_gpu_streams.py's workers do.)
-                for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
-                    if (!p->ik_busy[k] &&
-                        !(p->ik_ev[k] && p->ik_stream[k] == (void*)hipStreamPerThread && p->ik_thread[k] != self) &&
-                        (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess))
-                        set = k;
-                if (set >= 0) {
-                    if (!p->ik_ev[set] && hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming) != hipSuccess) {
-                        p->ik_ev[set] = nullptr;
-                        set = -1;
-                    } else {
-                        p->ik_busy[set] = true;
-                    }
-                } else {
-                    ++p->ik_one_phase_fallbacks;
+                bool waited = false;
+                for (;;) {
+                    int lru = -1;
+                    for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
+                        if (!p->ik_busy[k] && !per_thread && p->ik_ev[k] && p->ik_stream[k] == stream) set = k;
+                    for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
+                        if (!p->ik_busy[k] && (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess)) set = k;
+                    for (int k = 0; k < kin_plan::kIkEagerSets; ++k)
+                        if (!p->ik_busy[k] && (lru < 0 || p->ik_tick[k] < p->ik_tick[lru])) lru = k;
+                    if (set < 0) set = lru;
+                    if (set >= 0) break;
+                    // every set is between take and event record in other threads (a launch's host
+                    // time): wait for one rather than share it
+                    waited = true;
+                    p->ik_cv.wait(lk);
                 }
-            } else if (kin_plan::kIkEagerSets + p->ik_captured < kin_plan::kIkScratchSets)
+                if (waited) ++p->ik_stats.host_waits;
+                hipError_t ee = hipSuccess;
+                if (!p->ik_ev[set]) {
+                    ee = hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming);
+                    if (ee != hipSuccess) p->ik_ev[set] = nullptr;
+                } else if (per_thread || p->ik_stream[set] != stream) {
+                    // device-side order after the set's previous call, whichever stream or thread made it
+                    ee = hipStreamWaitEvent((hipStream_t)stream, p->ik_ev[set], 0);
+                    ++p->ik_stats.stream_waits;
+                }
+                if (ee != hipSuccess)
+                    return set_error(KIN_E_DEVICE, std::string("kin_ik_dls_batch: two-phase scratch ordering: ") +
+                                                       hipGetErrorString(ee));
+                p->ik_busy[set] = true;
+                p->ik_tick[set] = ++p->ik_ticks;
+                ++p->ik_stats.two_phase_calls;
+            } else if (kin_plan::kIkEagerSets + p->ik_captured < kin_plan::kIkScratchSets) {
                 set = kin_plan::kIkEagerSets + p->ik_captured++;
+                ++p->ik_stats.captured_calls;
+            } else {
+                ++p->ik_stats.captured_one_phase;
+            }
         }
         if (set >= 0 && !capturing) eager_set = set;
         if (set >= 0) {  // (no set left: one phase)
@@ -2073,13 +2086,15 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         e = launch_ik_dls<double>(p->pd, (const KStep<double>*)p->d_steps, p->geom, a, (const double*)target, ldt,
                                   (const double*)q0, (double*)q, ldq, n, iters, (double*)err, lde, jf, scr,
                                   (hipStream_t)stream);
-    if (eager_set >= 0) {  // the set is free again once this call has run on its stream
-        std::lock_guard<std::mutex> lk(p->ik_mu);
-        if (hipEventRecord(p->ik_ev[eager_set], (hipStream_t)stream) != hipSuccess)
-            (void)hipStreamSynchronize((hipStream_t)stream);  // (cannot tell when it finishes otherwise)
-        p->ik_stream[eager_set] = stream;
-        p->ik_thread[eager_set] = std::this_thread::get_id();
-        p->ik_busy[eager_set] = false;
+    if (eager_set >= 0) {  // the set's next call is ordered after this event (or after this stream's work)
+        {
+            std::lock_guard<std::mutex> lk(p->ik_mu);
+            if (hipEventRecord(p->ik_ev[eager_set], (hipStream_t)stream) != hipSuccess)
+                (void)hipStreamSynchronize((hipStream_t)stream);  // (the event then orders nothing: drain first)
+            p->ik_stream[eager_set] = stream;
+            p->ik_busy[eager_set] = false;
+        }
+        p->ik_cv.notify_one();
     }
     if (e != hipSuccess)
         return set_error(KIN_E_DEVICE, std::string("k_ik_dls launch: ") + hipGetErrorString(e) +
@@ -2106,6 +2121,13 @@ int kin_ik_dls_batch_trace(const kin_plan* p, const kin_ik_params* prm, const vo
                            void* stream) {
     if (!q0 || !trace) return set_error(KIN_E_INVALID, "kin_ik_dls_batch_trace: null q0 / trace");
     return ik_dls_batch(p, prm, target, ldt, q0 == q ? nullptr : q0, q, ldq, n, iters, nullptr, 0, stream, trace, ldtr);
+}
+
+int kin_plan_ik_sched_stats(const kin_plan* p, kin_ik_sched_stats* out) {
+    if (!p || !out) return set_error(KIN_E_INVALID, "kin_plan_ik_sched_stats: null plan / out");
+    std::lock_guard<std::mutex> lk(p->ik_mu);
+    *out = p->ik_stats;
+    return KIN_OK;
 }
 
 int kin_point_ik_nakamura_batch(const kin_plan* p, const void* pts, int64_t ldpt, void* q, int64_t ldq, int64_t n,

@@ -9,6 +9,11 @@
 #   inverse_kinematics!(m, link, ...)      src/inverse_kinematics.jl:23-30 -> inverse_kinematics!(hm, link, joints, targets, Q)
 #   point_inverse_kinematics_nakamura      src/algorithm.jl:116-131 -> point_inverse_kinematics_nakamura!(hm, link, joints, points, Q)
 #
+# and the reference's own single-target signatures, unchanged but for `hm` in place of `m`:
+#   inverse_kinematics!(hm, link, joints, target::Transform; ftol, with_rot) -> (q, :FTOL_REACHED | ...)
+#   inverse_kinematics!(hm, link, joints, target::Transform, sscc, sdf; use_bistage, ftol, with_rot) -> (q, status)
+#   compute_coll_dists(hm, sscc, joints, sdf), compute_coll_dists_and_grads(hm, sscc, joints, sdf; truncation_dist)
+#
 # Device arrays are AMDGPU.jl `ROCArray`s in Julia's column-major layout:
 #   Q :: ROCMatrix{T}(N, n_joints [+3 base])      (configuration index fastest)
 #   poses :: ROCArray{T,3}(N, 12, n_links)        (3x4 column-major per link)
@@ -371,6 +376,10 @@ function HIPSDF(sdf::Kinematics.AbstractSDF)
     poses = Float64[]
     widths = Float64[]
     for b in boxes
+        # a box of UnionSDF(mechanism) (src/sdf.jl:82-97) is attached to a link of the scene: its world pose is
+        # written into b.pose by the SdfLinkType get_transform override (:14-20), which inv_pose runs when
+        # the link is not cached (:24-32) -- so the snapshot is the box at the scene's current angles
+        Kinematics.inv_pose(b)
         append!(poses, vec(Matrix(b.pose.mat)))
         append!(widths, collect(b.width))
     end
@@ -450,6 +459,26 @@ function compute_coll_dists_and_grads!(hm::HIPModel, sscc::Kinematics.SweptSpher
     vals, grads
 end
 
+"""Cached kin_coll_ik_plan_create plan: the IK plan of `link` over `joints` with the checker's spheres."""
+function collik_plan!(hm::HIPModel, ::Type{T}, sscc::Kinematics.SweptSphereCollisionChecker, link::Link,
+                      joints::Vector{<:Joint}) where {T}
+    ids = Int32[j.id for j in joints]
+    sph = Int32[l.id for l in sscc.sphere_links]
+    key = (:collik, T, ids, sph, link.id)
+    cached_plan!(hm, key, ids) do
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        r = Float64.(sscc.sphere_radii)
+        GC.@preserve ids sph r begin
+            d = KinCollDesc(dtype_code(T), length(ids), pointer(ids), length(sph), isempty(sph) ? C_NULL : pointer(sph),
+                            C_NULL, isempty(r) ? C_NULL : pointer(r))
+            check(ccall((:kin_coll_ik_plan_create, libkinhip), Cint,
+                        (Ptr{Cvoid}, Ref{KinCollDesc}, Int32, Ref{Ptr{Cvoid}}), hm.handle, d, Int32(link.id), h))
+        end
+        hm.specialize && ccall((:kin_plan_specialize, libkinhip), Cint, (Ptr{Cvoid}, UInt32), h[], UInt32(0))
+        h[]
+    end
+end
+
 """Batched collision-aware IK, inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
 (src/inverse_kinematics.jl:1-21) for every row of `targets` (N, 12): stage 1 the collision-free DLS
 (kin_ik_dls_batch_from, seeds Q0), stage 2 the IneqConst(sscc, joints, sdf, 1, margin) sphere rows, both on
@@ -466,20 +495,7 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
                                         scene_q=nothing) where {T}
     sdf.attached && scene_q === nothing && throw(ArgumentError("an attached HIPSDF needs scene_q"))
     N = size(Q0, 1)
-    ids = Int32[j.id for j in joints]
-    sph = Int32[l.id for l in sscc.sphere_links]
-    key = (:collik, T, ids, sph, link.id)
-    p = cached_plan!(hm, key, ids) do
-        h = Ref{Ptr{Cvoid}}(C_NULL)
-        r = Float64.(sscc.sphere_radii)
-        GC.@preserve ids sph r begin
-            d = KinCollDesc(dtype_code(T), length(ids), pointer(ids), length(sph), pointer(sph), C_NULL, pointer(r))
-            check(ccall((:kin_coll_ik_plan_create, libkinhip), Cint,
-                        (Ptr{Cvoid}, Ref{KinCollDesc}, Int32, Ref{Ptr{Cvoid}}), hm.handle, d, Int32(link.id), h))
-        end
-        hm.specialize && ccall((:kin_plan_specialize, libkinhip), Cint, (Ptr{Cvoid}, UInt32), h[], UInt32(0))
-        h[]
-    end
+    p = collik_plan!(hm, T, sscc, link, joints)
     Q1 = similar(Q0)
     Q = similar(Q0)
     iters = ROCVector{Int32}(undef, N)
@@ -512,6 +528,134 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
                 N, pointer(iters), pointer(err), N, stream_ptr()))
     Q, iters, err
 end
+
+# --- the reference's own single-target calls (src/inverse_kinematics.jl:1-30, src/collision.jl:51-103) ---
+# Same signatures and return values as Kinematics.jl, so call sites and tests stay as they are (with `hm`,
+# the HIPModel of the Mechanism, in place of `m`): (q, status) with the reference's NLopt status symbols, the
+# mechanism's angles left at the answer.  fp64 throughout (the reference's precision).
+
+"""The 3x4 column-major 12-vector of a Transform (the C-ABI's target layout), as a (1, 12) device batch."""
+target_batch(T::Transform) = ROCMatrix{Float64}(reshape(Float64[T.mat[r, c] for c in 1:4 for r in 1:3], 1, 12))
+
+"""The mechanism's current angles of `joints` (+ base) as a (1, dof) device batch (get_joint_angles,
+src/mechanism.jl:203-221)."""
+angles_batch(m::Mechanism, joints::Vector{<:Joint}) = ROCMatrix{Float64}(reshape(get_joint_angles(m, joints), 1, :))
+
+"""inverse_kinematics!(m, link, joints, target; ftol, with_rot) (src/inverse_kinematics.jl:23-30) on the GPU ->
+(q, status).  The reference's objective (f_objective, :38-50: |[p* - p; rpy* - rpy]|^2 with the rpy_jac
+Jacobian; position only when !with_rot) minimised by damped least squares from the mechanism's current
+angles, stopped by the reference's ftol_abs rule -- NLopt stops when one step changes the objective by less
+than ftol (:62) -- checked on every iterate: one launch of max_iters steps records every iterate's residual
+(kin_ik_dls_batch_trace), the stopping iterate k is one launch of k steps from the same angles
+(kin_ik_dls_batch_from).  :FTOL_REACHED when the rule stopped it, :MAXEVAL_REACHED after max_iters steps.
+Sets the mechanism's angles to the answer.  Python mirror: kinhip.inverse_kinematics_ (mechanism.py)."""
+function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, target_pose::Transform;
+                                        ftol=1e-5, with_rot=true, max_iters=200, lambda=1e-2, max_step=0.5)
+    m = hm.m
+    ids = Int32[j.id for j in joints]
+    p = plan!(hm, Float64, ids, Int32[link.id], Int32(link.id), ids, KIN_WITH_ROT)
+    tgt = target_batch(target_pose)
+    q0 = angles_batch(m, joints)
+    q = similar(q0)
+    iters = ROCVector{Int32}(undef, 1)
+    M = Int(max_iters)
+    mode = with_rot ? Int32(2) : Int32(0)
+    trace = fill!(ROCMatrix{Float64}(undef, 1, 2 * (M + 1)), NaN)  # [|dp|, |d rpy|] of iterates 0..M
+    prm = KinIkParams(M, lambda, 0.0, 0.0, max_step, mode, 0, 0, 1, 0, 0.0)
+    check(ccall((:kin_ik_dls_batch_trace, libkinhip), Cint,
+                (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Int64, Int64,
+                 Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
+                p, prm, pointer(tgt), 1, pointer(q0), pointer(q), 1, 1, pointer(iters), pointer(trace), 1, stream_ptr()))
+    tr = Array(trace)
+    f = tr[1, 1:2:end] .^ 2 .+ tr[1, 2:2:end] .^ 2  # the objective sum(pose_diff.^2) of iterates 0..M
+    status, k = :MAXEVAL_REACHED, M
+    for kk in 1:M
+        if abs(f[kk] - f[kk+1]) < ftol
+            status, k = :FTOL_REACHED, kk
+            break
+        end
+    end
+    prm_k = KinIkParams(k, lambda, 0.0, 0.0, max_step, mode, 0, 0, 1, 0, 0.0)
+    check(ccall((:kin_ik_dls_batch_from, libkinhip), Cint,
+                (Ptr{Cvoid}, Ref{KinIkParams}, Ptr{Float64}, Int64, Ptr{Float64}, Ptr{Float64}, Int64, Int64,
+                 Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
+                p, prm_k, pointer(tgt), 1, pointer(q0), pointer(q), 1, 1, pointer(iters), C_NULL, 1, stream_ptr()))
+    qv = vec(Array(q))
+    set_joint_angles(m, joints, qv)
+    qv, status
+end
+
+"""inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage, ftol, with_rot)
+(src/inverse_kinematics.jl:1-21) on the GPU -> (q, status).  Stage 1 (use_bistage) is the collision-free
+call above (it moves the mechanism to its answer, as the reference's NLopt stage 1 does through
+f_objective's set_joint_angles); stage 2 solves the same objective subject to IneqConst(sscc, joints, sdf, 1,
+margin)'s sphere distances (:16-17) and the joint limits from the mechanism's current angles: the batched
+kin_ik_coll_batch kernel on a batch of one, 3 seeded restarts, converged when |dp|, |d rpy| < 1e-6 with every
+sphere at >= margin - 1e-6 (:FTOL_REACHED); otherwise the attempt of lowest merit, :MAXEVAL_REACHED.  `sdf`
+is the reference's UnionSDF / BoxSDF (a snapshot at the scene's current angles, HIPSDF(sdf)) or a HIPSDF; an
+attached HIPSDF(scene, joints) takes `scene_q`, its scene column values (a ROCVector).  A checker without
+spheres (the reference's own PR2 test adds none: test/test_inverse_kinematics.jl:63 is an un-iterated
+generator) leaves stage 2 an unconstrained solve.  Python mirror: kinhip.planning.collision_aware_ik."""
+function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, target_pose::Transform,
+                                        sscc::Kinematics.SweptSphereCollisionChecker,
+                                        sdf::Union{HIPSDF,Kinematics.AbstractSDF}; use_bistage=true, ftol=1e-5,
+                                        with_rot=true, max_iters=200, lambda=1e-2, max_step=0.5, margin=0.02,
+                                        scene_q=nothing)
+    m = hm.m
+    m === sscc.mech || throw(ArgumentError("the HIPModel must be the checker's mechanism (sscc.mech)"))
+    if use_bistage  # stage 1 seeds stage 2 (src/inverse_kinematics.jl:8-13)
+        Kinematics.inverse_kinematics!(hm, link, joints, target_pose; ftol=ftol, with_rot=with_rot,
+                                       max_iters=max_iters, lambda=lambda, max_step=max_step)
+    end
+    hs = sdf isa HIPSDF ? sdf : HIPSDF(sdf)
+    hs.attached && scene_q === nothing && throw(ArgumentError("an attached HIPSDF needs scene_q"))
+    p = collik_plan!(hm, Float64, sscc, link, joints)
+    tgt = target_batch(target_pose)
+    q0 = angles_batch(m, joints)
+    q = similar(q0)
+    iters = ROCVector{Int32}(undef, 1)
+    err = ROCMatrix{Float64}(undef, 1, 3)
+    prm = KinIkParams(max_iters, lambda, 1e-6, 1e-6, max_step, with_rot ? Int32(2) : Int32(0), 3, 0, 0, 0, 0.0)
+    cprm = KinIkCollParams(margin, 0.0, 1.0, 1e-6)
+    if hs.attached
+        check(ccall((:kin_ik_coll_batch_scene, libkinhip), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{Float64}, Int64, Ptr{Float64},
+                     Int64, Ptr{Float64}, Ptr{Float64}, Int64, Int64, Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
+                    p, hs.handle, prm, cprm, pointer(tgt), 1, pointer(scene_q), 0, pointer(q0), pointer(q), 1, 1,
+                    pointer(iters), pointer(err), 1, stream_ptr()))
+    else
+        check(ccall((:kin_ik_coll_batch, libkinhip), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{Float64}, Int64, Ptr{Float64},
+                     Ptr{Float64}, Int64, Int64, Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
+                    p, hs.handle, prm, cprm, pointer(tgt), 1, pointer(q0), pointer(q), 1, 1, pointer(iters),
+                    pointer(err), 1, stream_ptr()))
+    end
+    qv = vec(Array(q))
+    set_joint_angles(m, joints, qv)
+    qv, (Array(iters)[1] <= max_iters ? :FTOL_REACHED : :MAXEVAL_REACHED)
+end
+
+"""compute_coll_dists_and_grads(sscc, joints, sdf; truncation_dist) (src/collision.jl:96-103) at the mechanism's
+current angles -> (vals (n_spheres), grads (n_dof, n_spheres)), the GPU batch of one.  `sdf`: the reference's
+UnionSDF / BoxSDF or a HIPSDF (attached: `scene_q`)."""
+function Kinematics.compute_coll_dists_and_grads(hm::HIPModel, sscc::Kinematics.SweptSphereCollisionChecker,
+                                                 joints::Vector{<:Joint}, sdf::Union{HIPSDF,Kinematics.AbstractSDF};
+                                                 truncation_dist=Inf, scene_q=nothing, with_grad=true)
+    n = length(sscc.sphere_links)
+    n_dof = length(joints) + (hm.m.with_base ? 3 : 0)
+    n == 0 && return Float64[], zeros(n_dof, 0)
+    hs = sdf isa HIPSDF ? sdf : HIPSDF(sdf)
+    Q = angles_batch(hm.m, joints)
+    vals = ROCMatrix{Float64}(undef, 1, n)
+    grads = with_grad ? ROCArray{Float64}(undef, 1, n_dof, n) : nothing
+    compute_coll_dists_and_grads!(hm, sscc, joints, hs, Q, vals, grads; truncation_dist=truncation_dist, scene_q=scene_q)
+    vec(Array(vals)), (with_grad ? Array(grads)[1, :, :] : nothing)
+end
+
+"""compute_coll_dists(sscc, joints, sdf) (src/collision.jl:60-65) at the mechanism's current angles."""
+Kinematics.compute_coll_dists(hm::HIPModel, sscc::Kinematics.SweptSphereCollisionChecker, joints::Vector{<:Joint},
+                              sdf::Union{HIPSDF,Kinematics.AbstractSDF}; scene_q=nothing) =
+    Kinematics.compute_coll_dists_and_grads(hm, sscc, joints, sdf; scene_q=scene_q, with_grad=false)[1]
 
 """IneqConst over every waypoint column of Xi (N = waypoints of one or many trajectories, rows = dof):
 vals (N, n_coll) = min(dist, margin + 0.05) - margin, jac (N, n_dof, n_coll)."""

@@ -41,7 +41,7 @@ EXPORTS = [
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
     "kin_ineq_const_batch", "kin_pose_const_batch",
     "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
-    "kin_coll_batch_scene",
+    "kin_coll_batch_scene", "kin_plan_ik_sched_stats",
 ]
 
 
@@ -77,6 +77,12 @@ class IkParams(C.Structure):
                 ("tol_rot", C.c_double), ("max_step", C.c_double), ("with_rot", C.c_int32),
                 ("restarts", C.c_int32), ("seed", C.c_uint64), ("lanes", C.c_int32), ("index_base", C.c_int64),
                 ("damp_err", C.c_double)]
+
+
+class IkSchedStats(C.Structure):
+    _fields_ = [("two_phase_calls", C.c_uint64), ("stream_waits", C.c_uint64), ("host_waits", C.c_uint64),
+                ("one_phase_fallbacks", C.c_uint64), ("captured_calls", C.c_uint64),
+                ("captured_one_phase", C.c_uint64)]
 
 
 class IkCollParams(C.Structure):
@@ -140,14 +146,18 @@ def lib():
         "kin_coll_batch_scene": ([P, P, C.c_double, P, I64, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
         "kin_ik_coll_batch": ([P, P, P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_ik_coll_batch_scene": ([P, P, P, P, P, I64, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
+        "kin_plan_ik_sched_stats": ([P, P], C.c_int),
     }
+    # KINHIP_LIB may name a tools-only build (tools/ab.py); KINHIP_SKIP_ABI_CHECK=1 is the explicit opt-out
+    # for builds of older sources (tools/ikc_fault_probe.py) that lack newer entry points
+    skip_abi = os.environ.get("KINHIP_SKIP_ABI_CHECK") == "1"
     for name, (args, res) in sig.items():
-        if os.environ.get("KINHIP_LIB") and not hasattr(L, name):
-            continue  # tools-only builds of older sources (tools/ikc_fault_probe.py) lack newer entries
+        if skip_abi and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    if not os.environ.get("KINHIP_LIB") and L.kin_abi_version() != ABI_VERSION:
+    if not skip_abi and L.kin_abi_version() != ABI_VERSION:
         raise KinError(KIN_E_INVALID, f"{LIB_PATH}: C-ABI version {L.kin_abi_version()}, this binding needs "
                                       f"{ABI_VERSION} (kin_ik_params layout); rebuild the library")
     _lib = L

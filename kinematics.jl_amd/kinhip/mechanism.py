@@ -266,6 +266,12 @@ class Plan:
         K.check(K.lib().kin_plan_specialized(self._h, C.byref(v)))
         return v.value
 
+    def ik_sched_stats(self) -> dict:
+        """kin_plan_ik_sched_stats: counters of the two-phase IK scratch-set scheduling (tests)."""
+        st = K.IkSchedStats()
+        K.check(K.lib().kin_plan_ik_sched_stats(self._h, C.byref(st)))
+        return {name: int(getattr(st, name)) for name, _ in K.IkSchedStats._fields_}
+
     def _check_q(self, Q: torch.Tensor) -> int:
         if not Q.is_cuda or Q.dtype != self.dtype or Q.dim() != 2 or Q.shape[0] != self.n_qcols:
             raise ValueError(f"Q must be a CUDA {self.dtype} tensor of shape ({self.n_qcols}, N)")

@@ -1,9 +1,13 @@
-"""Two host threads on hipStreamPerThread: the handle ((hipStream_t)2) names each calling
-thread's own default stream, so the two-phase IK's "same stream as last time" shortcut must not hand one
-thread's in-flight scratch set (hand-over rings, fail lists) to the other.  Both threads run config-4 sized
-batches (two-phase schedule) back to back on that handle, each into its own outputs; every result must
-equal the single-threaded reference bit for bit.  The same with one explicit stream per thread, and with
-one thread on the per-thread handle, as controls."""
+"""Host threads on hipStreamPerThread (VERDICT r05 "next" 1).  The handle ((hipStream_t)2)
+names each calling thread's own default stream, so the two-phase IK's scratch sets (hand-over rings, fail
+lists) may be taken by calls on different streams.  Since round 6 every call that takes a set is ordered
+after the set's previous call on the device (hipStreamWaitEvent on the set's event, kinhip_host.cpp), so
+any number of threads, streams or handles share the 4 sets without ever running two calls in one set.
+
+Every result must equal the single-threaded reference bit for bit.  How a test may READ a worker's results
+follows the runtime rule tools/pts_probe.hip measured (profiles/r06_pts_probe.txt): hipDeviceSynchronize on
+the main thread does not wait for work an EXITED thread left on its per-thread stream, so a worker either
+synchronizes its stream before it ends or records an event there that the main thread waits on."""
 import ctypes as C
 import os
 import threading
@@ -41,16 +45,32 @@ def config4():
 
 
 def _hip():
-    return C.CDLL("libamdhip64.so.7")  # (the runtime torch has loaded: same soname, same instance)
+    h = C.CDLL("libamdhip64.so.7")  # (the runtime torch has loaded: same soname, same instance)
+    h.hipEventCreateWithFlags.argtypes = [C.c_void_p, C.c_uint]
+    h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+    h.hipEventSynchronize.argtypes = [C.c_void_p]
+    h.hipEventDestroy.argtypes = [C.c_void_p]
+    h.hipStreamSynchronize.argtypes = [C.c_void_p]
+    return h
 
 
-def _run(config4, n_threads, streams, reps=6, sync_in_thread=True):
+def _run(config4, n_threads, streams, reps=6, sync="stream", concurrent=True):
+    """n_threads workers, worker t on streams[t], reps IK calls each into its own outputs.
+    sync: "stream" -- the worker synchronizes its stream before it ends;
+          "event"  -- the worker only records an event on its stream, the main thread waits on it after join;
+          "device" -- nothing in the worker; the main thread's device-wide synchronize only (valid for
+                      streams that outlive the workers, i.e. not for per-thread streams: module doc).
+    concurrent=False runs the workers one after another (each joined before the next starts)."""
     dev, plan, tgt, Q0, ref_q, ref_it, N = config4
     prm = K.IkParams(64, 1e-2, 1e-3, 1e-3, 0.5, 1, 3, 0, 0, 0, 0.0)
     outs = [[(torch.empty_like(Q0), torch.empty(N, dtype=torch.int32, device=dev)) for _ in range(reps)]
             for _ in range(n_threads)]
+    hip = _hip()
+    events = [C.c_void_p() for _ in range(n_threads)]
+    for ev in events:
+        assert hip.hipEventCreateWithFlags(C.byref(ev), 2) == 0  # hipEventDisableTiming
     errors = []
-    barrier = threading.Barrier(n_threads)
+    barrier = threading.Barrier(n_threads if concurrent else 1)
 
     def worker(t):
         try:
@@ -60,34 +80,88 @@ def _run(config4, n_threads, streams, reps=6, sync_in_thread=True):
             for Q, it in outs[t]:
                 K.check(K.lib().kin_ik_dls_batch_from(plan._h, C.byref(prm), tgt.data_ptr(), N, Q0.data_ptr(),
                                                       Q.data_ptr(), N, N, it.data_ptr(), None, N, st))
-            # a thread's per-thread default stream is its own: the thread waits for it before it ends (the
-            # device-wide synchronize below does not cover the streams of threads that have exited)
-            if sync_in_thread:
-                assert _hip().hipStreamSynchronize(st) == 0
+            if sync == "stream":
+                assert hip.hipStreamSynchronize(st) == 0
+            elif sync == "event":
+                assert hip.hipEventRecord(events[t], st) == 0
         except Exception as e:  # noqa: BLE001 (reported below)
             errors.append(e)
 
     th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
-    for x in th:
-        x.start()
-    for x in th:
-        x.join(timeout=120)
+    if concurrent:
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+    else:
+        for x in th:
+            x.start()
+            x.join(timeout=120)
+    if sync == "event":
+        for ev in events:
+            assert hip.hipEventSynchronize(ev) == 0
     torch.cuda.synchronize()
+    for ev in events:
+        hip.hipEventDestroy(ev)
     assert not errors, errors
-    bad = [[int((it != ref_it).sum()) + int((Q != ref_q).any(0).sum()) for Q, it in outs[t]] for t in range(n_threads)]
-    return bad
+    return [[int((it != ref_it).sum()) + int((Q != ref_q).any(0).sum()) for Q, it in outs[t]]
+            for t in range(n_threads)]
 
 
-def test_two_threads_on_the_per_thread_stream_handle(config4, reps=int(os.environ.get("STREAMS_REPS", "6"))):
+def _clean(bad):
+    return all(b == 0 for row in bad for b in row)
+
+
+def test_controls_one_thread_and_own_streams(config4):
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    controls = {"one thread, per-thread handle": _run(config4, 1, [HIP_STREAM_PER_THREAD], reps),
-                "two threads, own streams": _run(config4, 2, [s1.cuda_stream, s2.cuda_stream], reps)}
-    got = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps)
-    # (diagnostic, not asserted: without the in-thread synchronize, whether the device-wide one after
-    # the threads have ended covers their per-thread streams)
-    nosync = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps, sync_in_thread=False)
-    print("mismatching targets per call:", controls, "two threads, per-thread handle:", got,
-          "the same without the in-thread synchronize:", nosync)
-    for name, bad in controls.items():
-        assert all(b == 0 for row in bad for b in row), (name, bad)
-    assert all(b == 0 for row in got for b in row), got
+    one = _run(config4, 1, [HIP_STREAM_PER_THREAD])
+    own = _run(config4, 2, [s1.cuda_stream, s2.cuda_stream], sync="device")
+    assert _clean(one), one
+    assert _clean(own), own
+
+
+@pytest.mark.parametrize("sync", ["stream", "event"])
+def test_two_threads_on_the_per_thread_stream_handle(config4, sync,
+                                                      reps=int(os.environ.get("STREAMS_REPS", "6"))):
+    """The round-5 failing configuration (two threads, per-thread handle, 6 back-to-back two-phase calls
+    each, no synchronize in the worker's loop), read in either of the two ways the runtime allows."""
+    plan = config4[1]
+    before = plan.ik_sched_stats()
+    got = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps, sync=sync)
+    after = plan.ik_sched_stats()
+    print("mismatching targets per call:", got, "sched stats delta:",
+          {k: after[k] - before[k] for k in after})
+    assert _clean(got), got
+    assert after["one_phase_fallbacks"] == before["one_phase_fallbacks"] == 0
+    assert after["two_phase_calls"] - before["two_phase_calls"] == 2 * reps
+
+
+def test_more_threads_than_scratch_sets_concurrently(config4):
+    """6 threads at once on the per-thread handle (more than the 4 sets): sets are shared in turn, each
+    call ordered after the set's previous one on the device; no call runs the one-phase schedule."""
+    plan = config4[1]
+    before = plan.ik_sched_stats()
+    got = _run(config4, 6, [HIP_STREAM_PER_THREAD] * 6, reps=3, sync="event")
+    after = plan.ik_sched_stats()
+    assert _clean(got), got
+    assert after["one_phase_fallbacks"] == 0
+    assert after["two_phase_calls"] - before["two_phase_calls"] == 18
+    assert after["stream_waits"] > before["stream_waits"]
+
+
+def test_exited_threads_leave_no_sets_behind(config4):
+    """8 threads created and joined one after another on the per-thread handle, none synchronizing (events
+    only): the round-5 policy reserved a set per such thread and ran every later call one phase once 4 had
+    exited; now no set belongs to a thread, so every call takes one."""
+    plan = config4[1]
+    before = plan.ik_sched_stats()
+    got = _run(config4, 8, [HIP_STREAM_PER_THREAD] * 8, reps=2, sync="event", concurrent=False)
+    after = plan.ik_sched_stats()
+    assert _clean(got), got
+    assert after["one_phase_fallbacks"] == 0
+    assert after["two_phase_calls"] - before["two_phase_calls"] == 16
+    # and an explicit-stream caller afterwards still runs two phases
+    s = torch.cuda.Stream()
+    got2 = _run(config4, 1, [s.cuda_stream], reps=2, sync="stream")
+    assert _clean(got2), got2
+    assert plan.ik_sched_stats()["two_phase_calls"] - after["two_phase_calls"] == 2

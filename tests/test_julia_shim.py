@@ -125,7 +125,7 @@ def test_julia_struct_mirrors_c_struct(jl_name):
 
 RUN_ENTRIES = ("kin_plan_run", "kin_plan_run_tiled", "kin_ik_dls_batch", "kin_ik_dls_batch_from",
                "kin_point_ik_nakamura_batch", "kin_coll_batch", "kin_ineq_const_batch", "kin_pose_const_batch",
-               "kin_coll_batch_scene", "kin_ik_coll_batch")
+               "kin_coll_batch_scene", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_ik_dls_batch_trace")
 
 
 def jl_functions(src):
@@ -149,12 +149,12 @@ def test_every_cached_plan_path_goes_through_the_staleness_check():
             for entry in RUN_ENTRIES:
                 if re.search(r"ccall\(\(:%s,\s*libkinhip\)" % entry, body):
                     runners += 1
-                    assert re.search(r"\b(plan!|coll_plan!|cached_plan!)\(hm,", body), (name, entry)
+                    assert re.search(r"\b(plan!|coll_plan!|collik_plan!|cached_plan!)\(hm,", body), (name, entry)
     assert runners >= 9
-    for name in ("plan!", "coll_plan!"):
+    for name in ("plan!", "coll_plan!", "collik_plan!"):
         (body,) = fns[name]
         assert "cached_plan!(hm, key," in body, name
-        assert "kin_plan_create" in body or "kin_coll_plan_create" in body
+        assert any(c in body for c in ("kin_plan_create", "kin_coll_plan_create", "kin_coll_ik_plan_create"))
     (cp,) = fns["cached_plan!"]
     assert cp.index("sync!(hm)") < cp.index("baked_angles(") < cp.index("hit[2] == baked")
     assert "kin_plan_destroy" in cp  # a stale plan is dropped, not reused
