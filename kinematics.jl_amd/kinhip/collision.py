@@ -366,8 +366,11 @@ def compute_coll_dists(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF)
 def compute_coll_dists_and_grads(sscc: SweptSphereCollisionChecker, joints, sdf: UnionSDF,
                                  truncation_dist=float("inf"), with_grad=True):
     """src/collision.jl:96-103: (vals [n_sph], grads [n_dof, n_sph])."""
-    dev = _device()
     m = sscc.mech
+    if not sscc.sphere_links:  # (the reference's own PR2 test builds a checker without spheres)
+        n_dof = len(joints) + (3 if m.with_base else 0)
+        return np.zeros(0), (np.zeros((n_dof, 0)) if with_grad else None)
+    dev = _device()
     plan = CollisionPlan(sscc, joints, torch.float64)
     Q = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
     D, G, _ = plan.run(sdf, Q, dists=True, grads=with_grad, truncation=truncation_dist)

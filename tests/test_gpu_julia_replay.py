@@ -7,6 +7,11 @@ reference reads m.angles and the tree on every call (src/algorithm.jl:1-37), so 
 the oracle at the mechanism's state of that moment (1e-12, fp64).  A replay without sync! (the round-2
 shim) is run beside it to show the sequence does catch a stale plan.
 
+The shim's single-target calls -- the reference's own signatures inverse_kinematics!(hm, link, joints,
+target::Transform; ftol, with_rot) -> (q, status), its collision form (sscc, sdf; use_bistage) and
+compute_coll_dists -- are replayed the same way for all three testsets of test/test_inverse_kinematics.jl,
+asserting the reference's checks verbatim (VERDICT r05 "next" 2).
+
 Julia is not in this image; tests/test_julia_shim.py checks statically that every batched call of the
 shim obtains its plan through cached_plan! (and so through sync!)."""
 import ctypes as C
@@ -29,12 +34,26 @@ def _p(a):
 
 
 class Mech:
-    """The Julia Mechanism's state the shim reads: links / joints (kinhip's Python mirror as data) and
-    m.angles.  Its own C model is not used by the replay."""
+    """The Julia Mechanism's state the shim reads: links / joints (kinhip's Python mirror as data),
+    m.angles and m.base_pose.  Its own C model is not used by the replay."""
 
-    def __init__(self, path):
-        self.m = kinhip.parse_urdf(path)
+    def __init__(self, path, with_base=False):
+        self.m = kinhip.parse_urdf(path, with_base=with_base)
+        self.with_base = with_base
         self.angles = np.zeros(len(self.m.joints))
+        self.base_pose = np.zeros(3)
+
+    def get_joint_angles(self, ids):
+        """get_joint_angles(m, joints) (src/mechanism.jl:203-221): the joints' angles, then the base pose."""
+        return np.array([self.angles[i - 1] for i in ids] + (list(self.base_pose) if self.with_base else []))
+
+    def set_joint_angles(self, ids, q):
+        """set_joint_angles(m, joints, angles) (src/mechanism.jl:223-231)."""
+        q = np.asarray(q, np.float64)
+        for i, a in zip(ids, q[:len(ids)]):
+            self.angles[i - 1] = a
+        if self.with_base:
+            self.base_pose = q[len(ids):len(ids) + 3].copy()
 
     def add_new_link(self, name, parent, T):
         self.m.add_new_link(kinhip.Link(name), parent, T)
@@ -44,7 +63,7 @@ class Mech:
 def model_handle(mech):
     """KinematicsHIP.jl model_handle: kin_model_create + kin_model_set_angles(m.angles)."""
     arrs = mech.m._tree_arrays()
-    d = K.TreeDesc(len(mech.m.links), len(mech.m.joints), *[_p(a).value for a in arrs], 0)
+    d = K.TreeDesc(len(mech.m.links), len(mech.m.joints), *[_p(a).value for a in arrs], int(mech.with_base))
     h = C.c_void_p()
     K.check(K.lib().kin_model_create(C.byref(d), C.byref(h)))
     a = np.ascontiguousarray(mech.angles, np.float64)
@@ -113,6 +132,37 @@ class HIPModel:
             d = K.PlanDesc(K.KIN_F64, qj.size, _p(qj).value, outs.size, _p(outs).value, jl, jj.size, _p(jj).value,
                            flags)
             K.check(K.lib().kin_plan_create(self.handle, C.byref(d), C.byref(h)))
+            K.lib().kin_plan_specialize(h, 0)
+            return h
+
+        return self.cached_plan(make, key, qj)
+
+    def coll_plan(self, sph_ids, radii, qj):
+        """KinematicsHIP.jl coll_plan!: kin_coll_plan_create(KinCollDesc(Float64, ids, spheres, radii)) + specialise."""
+        qj, sph = np.ascontiguousarray(qj, np.int32), np.ascontiguousarray(sph_ids, np.int32)
+        r = np.ascontiguousarray(radii, np.float64)
+        key = ("coll", qj.tobytes(), sph.tobytes())
+
+        def make():
+            h = C.c_void_p()
+            d = K.CollDesc(K.KIN_F64, qj.size, _p(qj).value, sph.size, _p(sph).value, None, _p(r).value)
+            K.check(K.lib().kin_coll_plan_create(self.handle, C.byref(d), C.byref(h)))
+            K.lib().kin_plan_specialize(h, 0)
+            return h
+
+        return self.cached_plan(make, key, qj)
+
+    def collik_plan(self, sph_ids, radii, link_id, qj):
+        """KinematicsHIP.jl collik_plan!: kin_coll_ik_plan_create (NULL sphere arrays when there are none)."""
+        qj, sph = np.ascontiguousarray(qj, np.int32), np.ascontiguousarray(sph_ids, np.int32)
+        r = np.ascontiguousarray(radii, np.float64)
+        key = ("collik", qj.tobytes(), sph.tobytes(), link_id)
+
+        def make():
+            h = C.c_void_p()
+            d = K.CollDesc(K.KIN_F64, qj.size, _p(qj).value, sph.size, _p(sph).value if sph.size else None, None,
+                           _p(r).value if r.size else None)
+            K.check(K.lib().kin_coll_ik_plan_create(self.handle, C.byref(d), link_id, C.byref(h)))
             K.lib().kin_plan_specialize(h, 0)
             return h
 
@@ -302,3 +352,261 @@ def test_shim_collision_ik_with_attached_fridge():
     assert c.mean() > 0.8
     np.testing.assert_allclose(Q.cpu().numpy()[:, c], rq[:, c], atol=1e-7)
     np.testing.assert_allclose(err.cpu().numpy()[:, c], rerr[:, c], atol=1e-9)
+
+
+# ---- the reference's single-target calls (KinematicsHIP.jl "the reference's own single-target calls") ----
+
+def _dev():
+    return torch.device("cuda", 0)
+
+
+def target_batch(T):
+    """KinematicsHIP.jl target_batch: the 3x4 column-major 12-vector, a batch of one."""
+    T = np.asarray(T, np.float64)
+    return torch.tensor([T[r, c] for c in range(4) for r in range(3)], dtype=torch.float64, device=_dev()).reshape(12, 1)
+
+
+def angles_batch(mech, ids):
+    """KinematicsHIP.jl angles_batch: get_joint_angles(m, joints) as a batch of one."""
+    return torch.tensor(mech.get_joint_angles(ids), dtype=torch.float64, device=_dev()).reshape(-1, 1).contiguous()
+
+
+def ik_ftol(hm, link_id, ids, T, ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2, max_step=0.5):
+    """KinematicsHIP.jl inverse_kinematics!(hm, link, joints, target_pose::Transform; ftol, with_rot), line for
+    line: the trace launch, NLopt's ftol_abs rule on every iterate's objective, the launch of k steps."""
+    mech = hm.mech
+    p = hm.plan(ids, [link_id], link_id, ids, K.KIN_WITH_ROT)
+    tgt = target_batch(T)
+    q0 = angles_batch(mech, ids)
+    q = torch.empty_like(q0)
+    iters = torch.empty(1, dtype=torch.int32, device=_dev())
+    M = int(max_iters)
+    mode = 2 if with_rot else 0
+    trace = torch.full((2 * (M + 1), 1), float("nan"), dtype=torch.float64, device=_dev())
+    prm = K.IkParams(M, lam, 0.0, 0.0, max_step, mode, 0, 0, 1, 0, 0.0)
+    K.check(K.lib().kin_ik_dls_batch_trace(p, C.byref(prm), tgt.data_ptr(), 1, q0.data_ptr(), q.data_ptr(), 1, 1,
+                                           iters.data_ptr(), trace.data_ptr(), 1, None))
+    tr = trace[:, 0].cpu().numpy()
+    f = tr[0::2] ** 2 + tr[1::2] ** 2
+    status, k = ":MAXEVAL_REACHED", M
+    for kk in range(1, M + 1):
+        if abs(f[kk - 1] - f[kk]) < ftol:
+            status, k = ":FTOL_REACHED", kk
+            break
+    prm_k = K.IkParams(k, lam, 0.0, 0.0, max_step, mode, 0, 0, 1, 0, 0.0)
+    K.check(K.lib().kin_ik_dls_batch_from(p, C.byref(prm_k), tgt.data_ptr(), 1, q0.data_ptr(), q.data_ptr(), 1, 1,
+                                          iters.data_ptr(), None, 1, None))
+    qv = q[:, 0].cpu().numpy()
+    mech.set_joint_angles(ids, qv)
+    return qv, status
+
+
+def ik_coll(hm, link_id, ids, T, sscc, sdf_h, use_bistage=True, ftol=1e-5, with_rot=True, max_iters=200, lam=1e-2,
+            max_step=0.5, margin=0.02):
+    """KinematicsHIP.jl inverse_kinematics!(hm, link, joints, target_pose::Transform, sscc, sdf; use_bistage, ftol,
+    with_rot) for a static sdf (HIPSDF(UnionSDF) = kin_sdf_create_boxes), line for line.  `sscc` =
+    (sphere link ids, radii)."""
+    mech = hm.mech
+    if use_bistage:
+        ik_ftol(hm, link_id, ids, T, ftol=ftol, with_rot=with_rot, max_iters=max_iters, lam=lam, max_step=max_step)
+    sph, rad = sscc
+    p = hm.collik_plan(sph, rad, link_id, ids)
+    tgt = target_batch(T)
+    q0 = angles_batch(mech, ids)
+    q = torch.empty_like(q0)
+    iters = torch.empty(1, dtype=torch.int32, device=_dev())
+    err = torch.empty((3, 1), dtype=torch.float64, device=_dev())
+    prm = K.IkParams(max_iters, lam, 1e-6, 1e-6, max_step, 2 if with_rot else 0, 3, 0, 0, 0, 0.0)
+    cprm = K.IkCollParams(margin, 0.0, 1.0, 1e-6)
+    K.check(K.lib().kin_ik_coll_batch(p, sdf_h, C.byref(prm), C.byref(cprm), tgt.data_ptr(), 1, q0.data_ptr(),
+                                      q.data_ptr(), 1, 1, iters.data_ptr(), err.data_ptr(), 1, None))
+    qv = q[:, 0].cpu().numpy()
+    mech.set_joint_angles(ids, qv)
+    return qv, (":FTOL_REACHED" if int(iters[0]) <= max_iters else ":MAXEVAL_REACHED")
+
+
+def compute_coll_dists(hm, sscc, ids, sdf_h):
+    """KinematicsHIP.jl compute_coll_dists(hm, sscc, joints, sdf): coll_plan! + kin_coll_batch on a batch of one at
+    the mechanism's current angles; no spheres -> an empty vector."""
+    sph, rad = sscc
+    if len(sph) == 0:
+        return np.zeros(0)
+    p = hm.coll_plan(sph, rad, ids)
+    Q = angles_batch(hm.mech, ids)
+    vals = torch.empty((len(sph), 1), dtype=torch.float64, device=_dev())
+    K.check(K.lib().kin_coll_batch(p, sdf_h, float("inf"), Q.data_ptr(), 1, 1, vals.data_ptr(), 1, None, 1, None,
+                                   None))
+    return vals[:, 0].cpu().numpy()
+
+
+def _isapprox(x, y, atol):
+    """Julia's isapprox(x, y; atol) on vectors (rtol = 0 when atol > 0): norm(x - y) <= atol."""
+    return float(np.linalg.norm(np.asarray(x) - np.asarray(y))) <= atol
+
+
+def _pose2angles(T):
+    """test_inverse_kinematics.jl:44: RotZYX(rotation(pose)) -> [theta1, theta2, theta3] (yaw, pitch, roll)."""
+    return O.rpy(T)[::-1]
+
+
+def _oracle_pose(path, mech, ids, link_name):
+    """get_transform(mech, link) -- the reference's CPU path (the oracle) at the mechanism's state."""
+    tree = O.parse_urdf_tree(path)
+    om = O.OracleMech(tree, with_base=mech.with_base)
+    nz = [j.id for j in mech.m.joints[:len(tree.joint_names)] if mech.angles[j.id - 1] != 0.0]
+    if nz or mech.with_base:
+        om.set_joint_angles(nz, [mech.angles[i - 1] for i in nz] + (list(mech.base_pose) if mech.with_base else []))
+    return om.get_transform(tree.link_id(link_name))
+
+
+def _translation(T):
+    return np.asarray(T)[:3, 3]
+
+
+def _transform(t):
+    T = np.eye(4)
+    T[:3, 3] = t
+    return T
+
+
+def _reset_manip_pose(robot):
+    """reset_manip_pose (src/models.jl:59-70)."""
+    r, l, torso = kinhip.PR2_MANIP_POSE
+    ids = [robot.m.find_joint(n).id for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS + ["torso_lift_joint"]]
+    av = list(np.deg2rad(r)) + list(np.deg2rad(l)) + [torso] + ([0.0, 0.0, 0.0] if robot.with_base else [])
+    robot.set_joint_angles(ids, av)
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_replay_reference_ik_fetch(with_base):
+    """test/test_inverse_kinematics.jl:1-25, through the shim's inverse_kinematics!(hm, link, joints, target)."""
+    path = golden("fetch.urdf")
+    mech = Mech(path, with_base=with_base)
+    hm = HIPModel(mech)
+    try:
+        joints = [mech.m.find_joint(n).id for n in ARM]
+        link = mech.m.find_link("gripper_link").id
+        target_pose = _transform((0.3, -0.4, 1.2))
+        q_goal, status = ik_ftol(hm, link, joints, target_pose, with_rot=True)
+        assert status == ":FTOL_REACHED"
+        mech.set_joint_angles(joints, q_goal)
+        pose_now = _oracle_pose(path, mech, joints, "gripper_link")
+        assert _isapprox(O.rpy(pose_now), O.rpy(target_pose), atol=1e-3)
+        assert _isapprox(_translation(pose_now), _translation(target_pose), atol=1e-3)
+    finally:
+        hm.close()
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_replay_reference_ik_pr2_no_collision(with_base):
+    """test/test_inverse_kinematics.jl:29-50 (tests/golden/pr2_two_arms.urdf for load_pr2: network-only),
+    both with_rot calls in sequence on the same robot, ftol = 1e-7."""
+    path = golden("pr2_two_arms.urdf")
+    robot = Mech(path, with_base=with_base)
+    hm = HIPModel(robot)
+    try:
+        link = robot.m.find_link("l_gripper_tool_frame").id
+        joints = [robot.m.find_joint(n).id for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS]
+        _reset_manip_pose(robot)
+        pose_target = _transform((0.6, 0.7, 0.8))
+        for with_rot in (False, True):
+            _, status = ik_ftol(hm, link, joints, pose_target, with_rot=with_rot, ftol=1e-7)
+            assert status == ":FTOL_REACHED", with_rot
+            pose_actual = _oracle_pose(path, robot, joints, "l_gripper_tool_frame")
+            pos_diff = _translation(pose_target) - _translation(pose_actual)
+            assert np.linalg.norm(pos_diff) < 1e-3, (with_rot, pos_diff)
+            if with_rot and with_base:
+                rot_diff = _pose2angles(pose_target) - _pose2angles(pose_actual)
+                assert np.linalg.norm(rot_diff) < 1e-3, rot_diff
+    finally:
+        hm.close()
+
+
+def _fridge_scene():
+    """test_inverse_kinematics.jl:53-70: the fridge with its base, door 2.0 at base (1.2, 0, 0); the target
+    Transform((0, 0, 1.2)) * pose_fridge; sdf = UnionSDF(fridge) at that state (HIPSDF(sdf) snapshot)."""
+    fridge = kinhip.parse_urdf(golden("fridge.urdf"), with_base=True)
+    sdf = kinhip.fridge_sdf(fridge, door_angle=2.0, base=(1.2, 0.0, 0.0))  # kin_sdf_create_boxes of the boxes
+    ft = O.parse_urdf_tree(golden("fridge.urdf"))
+    of = O.OracleMech(ft, with_base=True)
+    of.set_joint_angles([ft.joint_id("door_joint")], [2.0, 1.2, 0.0, 0.0])
+    pose_fridge = of.get_transform(ft.link_id("base_link"))
+    pose_target = _transform((0.0, 0.0, 1.2)) @ pose_fridge
+    boxes = O.OracleUnionSDF(*O.fridge_boxes(ft, door_angle=2.0, base=(1.2, 0.0, 0.0)))
+    return sdf, pose_target, boxes
+
+
+@pytest.mark.parametrize("spheres", ["verbatim", "arm_spheres"])
+def test_replay_reference_ik_pr2_with_collision(spheres):
+    """test/test_inverse_kinematics.jl:52-86 through the shim's collision form and compute_coll_dists.
+    "verbatim": the reference's checker exactly as its test builds it -- `(add_coll_links(sscc, link) for link
+    in collision_links)` (:63) is an un-iterated generator, so no sphere is added and the constraint is
+    empty; "arm_spheres": the spheres that line means to add (kinhip.PR2_ARM_SPHERES on both arms' collision
+    links, build-defined: the reference fits them to meshes), so stage 2 enforces them.  The reference's own
+    checks: :FTOL_REACHED, norm(pos_diff) < 1e-3, norm(rot_diff) < 1e-3, all(compute_coll_dists .> -1e-5); the
+    distances also equal the oracle's at the answer."""
+    path = golden("pr2_two_arms.urdf")
+    sdf, pose_target, boxes = _fridge_scene()
+    robot = Mech(path, with_base=True)
+    sph, rad, par, centres = [], [], [], []
+    if spheres == "arm_spheres":
+        for name, c, r in kinhip.PR2_ARM_SPHERES:
+            robot.add_new_link(f"sphere_{len(sph)}", robot.m.find_link(name), _transform(c))
+            sph.append(robot.m.find_link(f"sphere_{len(sph)}").id)
+            rad.append(r)
+            par.append(name)
+            centres.append(c)
+    hm = HIPModel(robot)
+    try:
+        joints = [robot.m.find_joint(n).id for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS]
+        _reset_manip_pose(robot)
+        link = robot.m.find_link("l_gripper_tool_frame").id
+        q_goal, status = ik_coll(hm, link, joints, pose_target, (sph, rad), sdf._h, with_rot=True, use_bistage=True)
+        assert status == ":FTOL_REACHED"
+        pose_actual = _oracle_pose(path, robot, joints, "l_gripper_tool_frame")
+        pos_diff = _translation(pose_target) - _translation(pose_actual)
+        assert np.linalg.norm(pos_diff) < 1e-3, pos_diff
+        rot_diff = _pose2angles(pose_target) - _pose2angles(pose_actual)
+        assert np.linalg.norm(rot_diff) < 1e-3, rot_diff
+        vals = compute_coll_dists(hm, (sph, rad), joints, sdf._h)
+        assert np.all(vals > -1e-5), vals
+        assert vals.size == len(sph)
+        if sph:  # the same distances from the CPU restatement at the answer
+            tree = O.parse_urdf_tree(path)
+            om = O.OracleMech(tree, with_base=True)
+            osph = []
+            for name, c in zip(par, centres):
+                osph.append(om.add_new_link(tree.link_id(name), _transform(c)))
+            oids = [tree.joint_id(n) for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS]
+            om.set_joint_angles([tree.joint_id("torso_lift_joint")], [kinhip.PR2_MANIP_POSE[2], 0.0, 0.0, 0.0])
+            q = robot.get_joint_angles(joints).reshape(-1, 1)
+            od = O.coll_batch(om, boxes, q, oids, osph, rad)[0][:, 0]
+            np.testing.assert_allclose(vals, od, atol=1e-9)
+            print(f"arm spheres: min distance {vals.min():.4f} (margin 0.02)")
+    finally:
+        hm.close()
+
+
+@pytest.mark.parametrize("spheres", ["verbatim", "arm_spheres"])
+def test_python_mirror_reference_pr2_with_collision(spheres):
+    """The same reference testset through the Python mirror (kinhip.inverse_kinematics_ with kinhip.UnionSDF,
+    kinhip.compute_coll_dists), the reference's checks verbatim."""
+    sdf, pose_target, _ = _fridge_scene()
+    robot = kinhip.parse_urdf(golden("pr2_two_arms.urdf"), with_base=True)
+    joints = [robot.find_joint(n) for n in kinhip.PR2_RARM_JOINTS + kinhip.PR2_LARM_JOINTS]
+    sscc = kinhip.SweptSphereCollisionChecker(robot)
+    if spheres == "arm_spheres":
+        for name, c, r in kinhip.PR2_ARM_SPHERES:
+            sscc.add_coll_sphere(robot.find_link(name), c, r)
+    r, l, torso = kinhip.PR2_MANIP_POSE
+    robot.set_joint_angles(joints + [robot.find_joint("torso_lift_joint")],
+                           list(np.deg2rad(r)) + list(np.deg2rad(l)) + [torso, 0.0, 0.0, 0.0])
+    link = robot.find_link("l_gripper_tool_frame")
+    q_goal, status = kinhip.inverse_kinematics_(robot, link, joints, pose_target, sscc, sdf, with_rot=True,
+                                                use_bistage=True)
+    assert status == ":FTOL_REACHED"
+    pose_actual = kinhip.get_transform(robot, link)
+    assert np.linalg.norm(_translation(pose_target) - _translation(pose_actual)) < 1e-3
+    assert np.linalg.norm(_pose2angles(pose_target) - _pose2angles(pose_actual)) < 1e-3
+    vals = kinhip.compute_coll_dists(sscc, joints, sdf)
+    assert np.all(vals > -1e-5), vals

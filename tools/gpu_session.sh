@@ -25,6 +25,7 @@
 #   cik                         the f3 bistage IK leg split by stage, stage 2 on one lane vs 4 (tools/cik_bench.py)
 #   coll-dump                   the specialised collision source (A/B build, KINHIP_JIT_DUMP) for offline ISA
 #   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
+#   pr2-miss[=<n>]              tools/pr2_miss_study.py (PR2 collision-IK leg misses vs host SLSQP)
 #   pts-probe                   tools/pts_probe (hipStreamPerThread after thread exit vs hipDeviceSynchronize)
 set -u -o pipefail
 mkdir -p gpurun_out/prof
@@ -59,6 +60,11 @@ for step in "$@"; do
       timeout -k 10 400 env KINHIP_LIB=$AB KINHIP_JIT_CODE_DUMP=$PWD/gpurun_out/isa/jit KINHIP_JIT_DUMP=$PWD/gpurun_out/isa/src \
         python bench.py --no-cpu > gpurun_out/isa/bench_ab.json 2> gpurun_out/isa/bench_ab.err || { tail gpurun_out/isa/bench_ab.err; exit 9; }
       python tools/isa_check.py gpurun_out/isa/jit.*.co > gpurun_out/isa/isa_check.txt 2>&1; tail -3 gpurun_out/isa/isa_check.txt ;;
+    pr2-miss|pr2-miss=*)
+      n=${step#pr2-miss}; n=${n#=}; n=${n:-200}
+      timeout -k 10 900 python tools/pr2_miss_study.py $n > gpurun_out/pr2_miss_study.json 2> gpurun_out/pr2_miss_study.err \
+        || { tail -20 gpurun_out/pr2_miss_study.err; exit 11; }
+      cut -c1-1500 gpurun_out/pr2_miss_study.json ;;
     pts-probe)
       timeout -k 10 60 tools/pts_probe > gpurun_out/pts_probe.txt 2>&1; rc=$?; cat gpurun_out/pts_probe.txt
       [ $rc -eq 0 ] || exit 10 ;;
