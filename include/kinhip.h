@@ -399,6 +399,15 @@ KINHIP_API int kin_coll_batch(const kin_plan* p, const kin_sdf* sdf, double trun
 KINHIP_API int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncation, const void* q,
                                     int64_t ldq, const void* scene_q, int64_t lds, int64_t n, void* dists,
                                     int64_t ldd, void* grads, int64_t ldg, void* min_dist, void* stream);
+/* Compiles kin_coll_batch_scene's kernels of plan p (kin_coll_plan_create) with one attached union's
+ * tables -- its groups, the scene steps of each group's frame, the boxes -- as constants as well (hiprtc,
+ * gfx950; synchronous, cached per process by source).  A planar base and a joint about a coordinate
+ * axis then leave a group frame of a few lane values (the fridge: 10 instead of 24 registers) and the
+ * boxes' data are immediates.  Later kin_coll_batch_scene calls of p with this sdf run them; results are
+ * those of the other kernels (up to the sign of a zero).  The union is identified by the kin_sdf object:
+ * a new kin_sdf (even of the same scene) runs the plan's other kernels until it is specialised too.
+ * No reference counterpart (the reference evaluates one sphere at a time, src/collision.jl:67-94). */
+KINHIP_API int kin_plan_specialize_scene(kin_plan* p, const kin_sdf* sdf);
 
 
 /* ------------------------------------------------------------------------- */

@@ -47,7 +47,7 @@ template <typename T>
 hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                              const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
                              int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf,
-                             hipStream_t st) {
+                             const JitFns* jfs, hipStream_t st) {
     const Tiling tl{0xffffffffu, 0, 0, 0, 0};
     const size_t lds = grads && a.n_boxes <= kCollLdsBoxes ? (size_t)a.n_boxes * sizeof(KBox<T>) : 0;
     for (int64_t s0 = 0; s0 < n; s0 += kChunk) {
@@ -67,7 +67,9 @@ hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSp
         T* mc = min_dist ? min_dist + s0 : min_dist;
         // plan-specialised (kin_plan_specialize, KIN_SPEC_COLL): the 2-group kernel when the scene has at
         // most 2 moving groups (24 fewer registers for the per-lane group frames than the 4-group one)
-        const hipFunction_t jk = jf ? jf->coll_scene[grads ? 1 : 0][sl.ng <= 2 ? 0 : 1] : nullptr;
+        // kin_plan_specialize_scene (jfs): this union's tables compiled in as well
+        const hipFunction_t jsc = jfs ? jfs->coll_scene_c[grads ? 1 : 0] : nullptr;
+        const hipFunction_t jk = jsc ? jsc : jf ? jf->coll_scene[grads ? 1 : 0][sl.ng <= 2 ? 0 : 1] : nullptr;
         if (jk) {
             // the 2-group kernel keeps its lanes' group frames in LDS after the boxes (coll_body, SceneCtx)
             static const bool frames_lds = ab_env_int("KINHIP_SCENE_LDS", 0) != 0;  // (A/B build; see kinhip_jit.cpp)
@@ -155,7 +157,7 @@ hipError_t launch_coll(const KProg<T>& P, const KStep<T>* steps, const KSphere<T
     template hipError_t launch_coll_scene<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, \
                                              const LaunchGeom&, const CollArgs&, const SceneLaunch&, const T*,        \
                                              int64_t, int64_t, T*, int64_t, T*, int64_t, T*, const JitFns*,     \
-                                             hipStream_t);
+                                             const JitFns*, hipStream_t);
 KIN_INSTANTIATE(float)
 KIN_INSTANTIATE(double)
 

@@ -152,7 +152,7 @@ __device__ __forceinline__ void box_gradient(const KBox<T>* __restrict__ boxes, 
     const T mx = fmax(q[0], fmax(q[1], q[2]));
     if (mx > T(0)) {  // outside: d = |max(q, 0)|
         const T o[3] = {fmax(q[0], T(0)), fmax(q[1], T(0)), fmax(q[2], T(0))};
-        const T oo = o[0] * o[0] + o[1] * o[1] + o[2] * o[2];
+        const T oo = fma(o[0], o[0], fma(o[1], o[1], o[2] * o[2]));  // (explicit: every kernel variant rounds alike)
         T rn;  // fp32: hardware v_rsq_f32 (1 ulp) instead of the ~10-instruction IEEE division
         if constexpr (sizeof(T) == 4) rn = rsqrt_fast(oo);
         else rn = T(1) / sqrt_t(oo);
@@ -223,15 +223,17 @@ __host__ __device__ constexpr bool scene_frames_in_lds(int scene_groups) {
     return KINHIP_SCENE_LDS && sizeof(T) == 4 && scene_groups > 0 && scene_groups <= 2;
 }
 
-// rotation by th about the unit axis u (Rodrigues; the reference's UnitQuaternion(cos th/2, u sin th/2))
+// rotation by th about the unit axis u (Rodrigues; the reference's UnitQuaternion(cos th/2, u sin th/2)).
+// fmaz / mul0: with the axis a compile-time constant (kin_plan_specialize_scene) a coordinate axis leaves
+// the 2x2 block of c and s alone (the other products are structural zeros)
 template <typename T>
 __device__ __forceinline__ void axis_rotation(const T* __restrict__ u, T th, T (&R)[9]) {
     T s, c;
     sincos_t(th, &s, &c);
     const T v = T(1) - c, x = u[0], y = u[1], z = u[2];
-    R[0] = fma(x * x, v, c);     R[1] = fma(x * y, v, -z * s); R[2] = fma(x * z, v, y * s);
-    R[3] = fma(y * x, v, z * s); R[4] = fma(y * y, v, c);      R[5] = fma(y * z, v, -x * s);
-    R[6] = fma(z * x, v, -y * s); R[7] = fma(z * y, v, x * s); R[8] = fma(z * z, v, c);
+    R[0] = fmaz(x * x, v, c);              R[1] = fmaz(x * y, v, -mul0(z, s)); R[2] = fmaz(x * z, v, mul0(y, s));
+    R[3] = fmaz(y * x, v, mul0(z, s));     R[4] = fmaz(y * y, v, c);           R[5] = fmaz(y * z, v, -mul0(x, s));
+    R[6] = fmaz(z * x, v, -mul0(y, s));    R[7] = fmaz(z * y, v, mul0(x, s));  R[8] = fmaz(z * z, v, c);
 }
 
 // the group frames of this sample (get_transform(scene, link) up to the group's moving frame), inverted
@@ -261,22 +263,22 @@ __device__ __forceinline__ void scene_frames(SceneCtx<T, MAXG, LF>& sc, const Sc
                 for (int i = 0; i < 3; ++i)
 #pragma unroll
                     for (int j = 0; j < 3; ++j)
-                        h.r[3 * i + j] = fma(f.r[3 * i], R[j], fma(f.r[3 * i + 1], R[3 + j], f.r[3 * i + 2] * R[6 + j]));
+                        h.r[3 * i + j] = fmaz(f.r[3 * i], R[j], fmaz(f.r[3 * i + 1], R[3 + j], mul0z(f.r[3 * i + 2], R[6 + j])));
 #pragma unroll
                 for (int k2 = 0; k2 < 9; ++k2) f.r[k2] = h.r[k2];
             } else if (st.kind == MOT_PRISM) {
                 const T d = ld_soa(sa.q, st.qcol, sa.ld, so);
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
-                    f.t[i] = fma(fma(f.r[3 * i], st.axis[0], fma(f.r[3 * i + 1], st.axis[1], f.r[3 * i + 2] * st.axis[2])), d,
-                                 f.t[i]);
+                    f.t[i] = fma(fmaz(f.r[3 * i], st.axis[0], fmaz(f.r[3 * i + 1], st.axis[1], mul0z(f.r[3 * i + 2], st.axis[2]))),
+                                 d, f.t[i]);
             }
         }
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
 #pragma unroll
             for (int j = 0; j < 3; ++j) sc.set(g, 4 * i + j, f.r[3 * j + i]);
-            sc.set(g, 4 * i + 3, -fma(f.r[i], f.t[0], fma(f.r[3 + i], f.t[1], f.r[6 + i] * f.t[2])));
+            sc.set(g, 4 * i + 3, -fmaz(f.r[i], f.t[0], fmaz(f.r[3 + i], f.t[1], mul0z(f.r[6 + i], f.t[2]))));
         }
     }
 }
@@ -312,9 +314,9 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG, LF>& sc, con
         bool need = false;
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
-            lx[i] = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
-            ly[i] = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
-            lz[i] = fma(I[8], px[i], fma(I[9], py[i], fma(I[10], pz[i], I[11])));
+            lx[i] = fmaz(I[0], px[i], fmaz(I[1], py[i], fmaz(I[2], pz[i], I[3])));
+            ly[i] = fmaz(I[4], px[i], fmaz(I[5], py[i], fmaz(I[6], pz[i], I[7])));
+            lz[i] = fmaz(I[8], px[i], fmaz(I[9], py[i], fmaz(I[10], pz[i], I[11])));
             const T ox = fmax(fabs(lx[i] - (T)G.bc[0]) - (T)G.bh[0], T(0));
             const T oy = fmax(fabs(ly[i] - (T)G.bc[1]) - (T)G.bh[1], T(0));
             const T oz = fmax(fabs(lz[i] - (T)G.bc[2]) - (T)G.bh[2], T(0));
@@ -360,13 +362,13 @@ __device__ __forceinline__ void scene_union(const SceneCtx<T, MAXG, LF>& sc, con
                     for (int j = 0; j < 12; ++j) I[j] = wg[i] == g ? sc.inv[g][j] : I[j];
                 }
             }
-            const T lx = fma(I[0], px[i], fma(I[1], py[i], fma(I[2], pz[i], I[3])));
-            const T ly = fma(I[4], px[i], fma(I[5], py[i], fma(I[6], pz[i], I[7])));
-            const T lz = fma(I[8], px[i], fma(I[9], py[i], fma(I[10], pz[i], I[11])));
+            const T lx = fmaz(I[0], px[i], fmaz(I[1], py[i], fmaz(I[2], pz[i], I[3])));
+            const T ly = fmaz(I[4], px[i], fmaz(I[5], py[i], fmaz(I[6], pz[i], I[7])));
+            const T lz = fmaz(I[8], px[i], fmaz(I[9], py[i], fmaz(I[10], pz[i], I[11])));
             T gg[3];
             box_gradient<T>(boxes, smem, use_lds, wk[i], lx, ly, lz, gg);
 #pragma unroll
-            for (int j = 0; j < 3; ++j) gw[i][j] = fma(I[j], gg[0], fma(I[4 + j], gg[1], I[8 + j] * gg[2]));
+            for (int j = 0; j < 3; ++j) gw[i][j] = fmaz(I[j], gg[0], fmaz(I[4 + j], gg[1], mul0z(I[8 + j], gg[2])));
         }
     }
 }
@@ -556,7 +558,8 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
                                           const CollArgs& a, const T* __restrict__ q, int64_t ldq, int64_t n,
                                           T* __restrict__ dists, int64_t ldd, T* __restrict__ grads, int64_t ldg,
                                           T* __restrict__ min_dist, const Tiling& tl, unsigned char* smem,
-                                          const SceneArgs<T>& sa = SceneArgs<T>{}) {
+                                          const SceneArgs<T>& sa = SceneArgs<T>{},
+                                          const KAabb<T>* __restrict__ aabb_c = nullptr) {
     // gradient kernels: the union's KBox records into LDS (see kCollLdsBoxes); the launcher gives
     // the workgroup min(n_boxes, kCollLdsBoxes) * sizeof(KBox<T>) bytes
     const bool use_lds = GRAD && a.n_boxes <= kCollLdsBoxes;  // uniform
@@ -612,7 +615,8 @@ __device__ __forceinline__ void coll_body(const KProg<T>& P, const KStep<T>* __r
         ro[s][0] = ro[s][1] = ro[s][2] = T(0);
         rz[s][0] = rz[s][1] = rz[s][2] = T(0);
     }
-    const KAabb<T>* aabb = reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
+    // the KAabb table after the KBox array (aabb_c: a scene-specialised kernel's constant table)
+    const KAabb<T>* aabb = aabb_c ? aabb_c : reinterpret_cast<const KAabb<T>*>(boxes + a.n_boxes);
     coll_spheres<T, MAXA, GRAD, SCENE>(-1, P.sph_root0, P.sph_root1, f, P, S, sph, boxes, aabb, a.n_aabb, a.n_boxes, trunc,
                                        offs, broad, bnd, ro, rz, bx, by, off, dists, ldd, grads, ldg, dmin, smem, use_lds,
                                        &sc);

@@ -308,6 +308,19 @@ __device__ __forceinline__ T mul0(T a, T b) {
     if (__builtin_constant_p(a) && a == T(0)) return T(0);
     return a * b;
 }
+// acc + a * b with the term dropped when a or b is a compile-time zero: the scene tables of a
+// scene-specialised collision kernel (kin_plan_specialize_scene) fold a planar base's and a fixed-axis
+// joint's structural zeros out of the per-lane group frames.  fma(a, b, acc) otherwise.
+template <typename T>
+__device__ __forceinline__ T fmaz(T a, T b, T acc) {
+    if ((__builtin_constant_p(a) && a == T(0)) || (__builtin_constant_p(b) && b == T(0))) return acc;
+    return fma(a, b, acc);
+}
+template <typename T>
+__device__ __forceinline__ T mul0z(T a, T b) {
+    if ((__builtin_constant_p(a) && a == T(0)) || (__builtin_constant_p(b) && b == T(0))) return T(0);
+    return a * b;
+}
 
 // f <- f * F   (F: row-major 3x4 in uniform memory)
 template <typename T>

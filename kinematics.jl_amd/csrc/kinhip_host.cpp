@@ -176,6 +176,16 @@ struct kin_sdf {
     double bc[3] = {0, 0, 0}, bh[3] = {0, 0, 0};  // world-aligned box enclosing every box (broad phase, coll_body)
     void* d_f32 = nullptr;
     void* d_f64 = nullptr;
+    // host copies of an attached union's tables (kin_plan_specialize_scene compiles them in), and an id that
+    // is never reused (the plans' scene-specialised kernels are keyed by it)
+    uint64_t uid = 0;
+    std::vector<KSceneGroup> h_groups;
+    std::vector<KSceneStep<float>> h_ssf;
+    std::vector<KSceneStep<double>> h_ssd;
+    std::vector<KBox<float>> h_bf;
+    std::vector<KBox<double>> h_bd;
+    std::vector<KAabb<float>> h_af;
+    std::vector<KAabb<double>> h_ad;
     ~kin_sdf() {
         if (d_f32) (void)hipFree(d_f32);
         if (d_f64) (void)hipFree(d_f64);
@@ -242,7 +252,16 @@ struct kin_plan {
     std::vector<unsigned char> h_ikc_steps, h_ikc_sph;
     void* d_ikc = nullptr;
     size_t ikc_sph_off = 0;
+    // kin_plan_specialize_scene: k_coll_scene kernels with one attached union compiled in, by kin_sdf uid
+    mutable std::mutex scene_mu;
+    std::map<uint64_t, JitKernels*> scene_jit;
+    const JitFns* scene_fns(uint64_t uid) const {
+        std::lock_guard<std::mutex> lk(scene_mu);
+        const auto it = scene_jit.find(uid);
+        return it == scene_jit.end() ? nullptr : jit_fns(it->second);
+    }
     ~kin_plan() {
+        for (auto& kv : scene_jit) jit_destroy(kv.second);
         if (d_ikc) (void)hipFree(d_ikc);
         for (hipEvent_t e : ik_ev)
             if (e) (void)hipEventDestroy(e);
@@ -1125,6 +1144,44 @@ int kin_plan_specialize(kin_plan* p, uint32_t kernels) {
 
 int kin_jit_selfcheck(void) { return jit_selfcheck(); }
 
+int kin_plan_specialize_scene(kin_plan* p, const kin_sdf* sdf) {
+    auto bad = [](int code, const std::string& w) { return set_error(code, "kin_plan_specialize_scene: " + w); };
+    if (!p || !sdf) return bad(KIN_E_INVALID, "null plan / sdf");
+    if (!p->is_coll || p->is_coll_ik) return bad(KIN_E_UNSUPPORTED, "plan was not made by kin_coll_plan_create");
+    if (!sdf->attached) return bad(KIN_E_INVALID, "the kin_sdf is not attached to a scene");
+    if (const int rc = check_device(p->device, "kin_plan_specialize_scene", "the plan")) return rc;
+    if (const int rc = check_device(sdf->device, "kin_plan_specialize_scene", "the kin_sdf")) return rc;
+    auto one = [&](kin_plan* s) -> int {
+        {
+            std::lock_guard<std::mutex> lk(s->scene_mu);
+            if (s->scene_jit.count(sdf->uid)) return KIN_OK;
+        }
+        JitKernels* k = nullptr;
+        int rc;
+        if (s->dtype == KIN_F32) {
+            const JitScene js{sdf->h_groups.data(), (int)sdf->h_groups.size(), sdf->h_ssf.data(), (int)sdf->h_ssf.size(),
+                              sdf->h_bf.data(), (int)sdf->h_bf.size(), sdf->h_af.data(), (int)sdf->h_af.size(),
+                              sdf->scene_base_col};
+            rc = jit_build_scene<float>(s->pf, (const KStep<float>*)s->h_steps.data(), s->n_steps, s->geom.maxA,
+                                        s->h_sph.empty() ? nullptr : s->h_sph.data(), s->n_sph, js, &k);
+        } else {
+            const JitScene js{sdf->h_groups.data(), (int)sdf->h_groups.size(), sdf->h_ssd.data(), (int)sdf->h_ssd.size(),
+                              sdf->h_bd.data(), (int)sdf->h_bd.size(), sdf->h_ad.data(), (int)sdf->h_ad.size(),
+                              sdf->scene_base_col};
+            rc = jit_build_scene<double>(s->pd, (const KStep<double>*)s->h_steps.data(), s->n_steps, s->geom.maxA,
+                                         s->h_sph.empty() ? nullptr : s->h_sph.data(), s->n_sph, js, &k);
+        }
+        if (rc != KIN_OK) return rc;
+        std::lock_guard<std::mutex> lk(s->scene_mu);
+        if (!s->scene_jit.emplace(sdf->uid, k).second) jit_destroy(k);
+        return KIN_OK;
+    };
+    if (p->parts.empty()) return one(p);
+    for (auto& part : p->parts)
+        if (const int rc = one(part.get())) return rc;
+    return KIN_OK;
+}
+
 int kin_plan_specialized(const kin_plan* p, uint32_t* kernels) {
     if (!p || !kernels) return set_error(KIN_E_INVALID, "kin_plan_specialized: null argument");
     *kernels = p->jit_mask;
@@ -1395,6 +1452,8 @@ int kin_sdf_create_attached(const kin_model* scene, int32_t n_q, const int32_t* 
             hs[k].kind = steps[k].kind;
             hs[k].qcol = steps[k].qcol;
         }
+        if constexpr (sizeof(T) == 4) sd->h_ssf.assign(hs.begin(), hs.begin() + steps.size());
+        else sd->h_ssd.assign(hs.begin(), hs.begin() + steps.size());
         const size_t nb = sd->scene_steps_off + sizeof(KSceneStep<T>) * hs.size();
         hipError_t e = hipMalloc(dst, nb);
         if (e == hipSuccess) e = hipMemcpy(*dst, groups.data(), sizeof(KSceneGroup) * groups.size(), hipMemcpyHostToDevice);
@@ -1403,6 +1462,13 @@ int kin_sdf_create_attached(const kin_model* scene, int32_t n_q, const int32_t* 
                           hipMemcpyHostToDevice);
         return e;
     };
+    sd->h_groups = groups;
+    sd->h_bf = bf;
+    sd->h_bd = bd;
+    sd->h_af = af;
+    sd->h_ad = ad;
+    static std::atomic<uint64_t> sdf_uids{0};
+    sd->uid = ++sdf_uids;
     hipError_t e = hipGetDevice(&sd->device);
     if (e == hipSuccess) e = upload_boxes(&sd->d_f32, bf, af);
     if (e == hipSuccess) e = upload_boxes(&sd->d_f64, bd, ad);
@@ -1903,6 +1969,7 @@ int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncatio
         const kin_plan* s = p->parts.empty() ? p : p->parts[k].get();
         a.accumulate = k > 0;
         const JitFns* jf = soff ? jit_fns(s->jit) : nullptr;
+        const JitFns* jfs = soff ? s->scene_fns(sdf->uid) : nullptr;  // (kin_plan_specialize_scene)
         const void* sc = s->dtype == KIN_F32 ? sdf->d_scene_f32 : sdf->d_scene_f64;
         const SceneLaunch sl{sc, (const char*)sc + sdf->scene_steps_off, scene_q, lds, sdf->n_groups,
                              sdf->scene_base_col, lds == 0 ? 1 : 0};
@@ -1910,12 +1977,12 @@ int kin_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, double truncatio
         if (s->dtype == KIN_F32)
             e = launch_coll_scene<float>(s->pf, (const KStep<float>*)s->d_steps, (const KSphere<float>*)s->d_sph,
                                          (const KBox<float>*)sdf->d_f32, s->geom, a, sl, (const float*)q, ldq, n,
-                                         (float*)dists, ldd, (float*)grads, ldg, (float*)min_dist, jf,
+                                         (float*)dists, ldd, (float*)grads, ldg, (float*)min_dist, jf, jfs,
                                          (hipStream_t)stream);
         else
             e = launch_coll_scene<double>(s->pd, (const KStep<double>*)s->d_steps, (const KSphere<double>*)s->d_sph,
                                           (const KBox<double>*)sdf->d_f64, s->geom, a, sl, (const double*)q, ldq, n,
-                                          (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, jf,
+                                          (double*)dists, ldd, (double*)grads, ldg, (double*)min_dist, jf, jfs,
                                           (hipStream_t)stream);
         if (e != hipSuccess) return set_error(KIN_E_DEVICE, std::string("k_coll_scene launch: ") + hipGetErrorString(e));
     }

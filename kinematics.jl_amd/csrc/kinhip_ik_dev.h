@@ -38,6 +38,13 @@ namespace {
 #ifndef KINHIP_IK_F64_ITERS
 #define KINHIP_IK_F64_ITERS 3
 #endif
+// ... and with KINHIP_IK_F64SOLVE = 3 the fp64 solve everywhere when lambda^2 is below this: the
+// analysis above rests on lambda^2 = 1e-4 against the fp32 normal equations' ~eps |J|^2 = 2.4e-7; a smaller
+// damping (down to lambda = 0, which kin_ik_params accepts) leaves the fp32 factorisation of a near-singular
+// arm without that margin (NaN pivots at lambda = 0).  A uniform kernel argument: one path per wave.
+#ifndef KINHIP_IK_F32SOLVE_MIN_LAM2
+#define KINHIP_IK_F32SOLVE_MIN_LAM2 0.99e-4
+#endif
 // Contraction only inside one expression (a * b + c): the specialised kernels (hiprtc) fold constants
 // into the instruction stream, and fusing across statements would then differ from the generic ones
 #ifndef KINHIP_CONTRACT_FAST
@@ -818,7 +825,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         };
         if constexpr (sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3) {
             // fp64 for the first iterations of attempt 0 (the caller's q0), fp32 elsewhere (see the macro)
-            if (att == 0 && it < KINHIP_IK_F64_ITERS) damped_solve(double());
+            if ((att == 0 && it < KINHIP_IK_F64_ITERS) || a.lam2 < T(KINHIP_IK_F32SOLVE_MIN_LAM2)) damped_solve(double());
             else damped_solve(float());
         } else {
             damped_solve(typename ik_solve_type<sizeof(T) == 4 && KINHIP_IK_F64SOLVE != 1>::type());

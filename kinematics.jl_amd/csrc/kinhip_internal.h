@@ -55,6 +55,8 @@ struct JitFns {
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
     hipFunction_t coll_scene[2][2] = {};  // the same over an attached union [with gradients][up to 2 | 4 groups]
+    // the same with one attached union's tables compiled in (kin_plan_specialize_scene) [with gradients]
+    hipFunction_t coll_scene_c[2] = {};
     // collision-aware IK (k_ik_tree) [rows == 6][lanes: 0 = 1 x 1, 1 = 1 sphere lane x 4 attempt groups,
     // 2 = 16 sphere lanes x 1, 3 = 16 x 4] (kIktVariants)
     hipFunction_t ikt[2][4] = {};
@@ -147,7 +149,8 @@ struct SceneLaunch {
 template <typename T>
 hipError_t launch_coll_scene(const KProg<T>& P, const KStep<T>* steps, const KSphere<T>* sph, const KBox<T>* boxes,
                              const LaunchGeom& g, const CollArgs& a, const SceneLaunch& sl, const T* q, int64_t ldq,
-                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf, hipStream_t st);
+                             int64_t n, T* dists, int64_t ldd, T* grads, int64_t ldg, T* min_dist, const JitFns* jf,
+                             const JitFns* jfs, hipStream_t st);
 
 template <typename T>
 hipError_t launch_pose_residual(const T* poses, int64_t ldp, const T* target, int64_t ldt, int64_t n, int rows, T* vals,

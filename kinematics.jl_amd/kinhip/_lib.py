@@ -41,7 +41,7 @@ EXPORTS = [
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
     "kin_ineq_const_batch", "kin_pose_const_batch",
     "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
-    "kin_coll_batch_scene", "kin_plan_ik_sched_stats",
+    "kin_coll_batch_scene", "kin_plan_ik_sched_stats", "kin_plan_specialize_scene",
 ]
 
 
@@ -147,6 +147,7 @@ def lib():
         "kin_ik_coll_batch": ([P, P, P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_ik_coll_batch_scene": ([P, P, P, P, P, I64, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_plan_ik_sched_stats": ([P, P], C.c_int),
+        "kin_plan_specialize_scene": ([P, P], C.c_int),
     }
     # KINHIP_LIB may name a tools-only build (tools/ab.py); KINHIP_SKIP_ABI_CHECK=1 is the explicit opt-out
     # for builds of older sources (tools/ikc_fault_probe.py) that lack newer entry points

@@ -151,6 +151,14 @@ class CollisionPlan:
         K.check(K.lib().kin_plan_specialize(self._h, K.KIN_SPEC_COLL))
         return self
 
+    def specialize_scene(self, sdf: "AttachedUnionSDF") -> "CollisionPlan":
+        """kin_plan_specialize_scene: also compile this plan's scene kernels with `sdf`'s tables (groups,
+        scene steps, boxes) as constants; later ``run(sdf, ..., scene_q=...)`` calls use them.  Returns self."""
+        if not isinstance(sdf, AttachedUnionSDF):
+            raise TypeError("specialize_scene needs an AttachedUnionSDF")
+        K.check(K.lib().kin_plan_specialize_scene(self._h, sdf._h))
+        return self
+
     @property
     def specialized(self) -> int:
         v = C.c_uint32()

@@ -37,7 +37,7 @@ hipError_t launch_coll(const KProg<T>&, const KStep<T>*, const KSphere<T>*, cons
 template <typename T>
 hipError_t launch_coll_scene(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*, const LaunchGeom&,
                              const CollArgs&, const SceneLaunch&, const T*, int64_t, int64_t, T*, int64_t, T*, int64_t,
-                             T*, const JitFns*, hipStream_t) {
+                             T*, const JitFns*, const JitFns*, hipStream_t) {
     return hipErrorNoDevice;
 }
 template <typename T>
@@ -62,7 +62,7 @@ hipError_t launch_pose_residual(const T*, int64_t, const T*, int64_t, int64_t, i
     template hipError_t launch_coll_scene<T>(const KProg<T>&, const KStep<T>*, const KSphere<T>*, const KBox<T>*,   \
                                              const LaunchGeom&, const CollArgs&, const SceneLaunch&, const T*,        \
                                              int64_t, int64_t, T*, int64_t, T*, int64_t, T*, const JitFns*,      \
-                                             hipStream_t);                                                            \
+                                             const JitFns*, hipStream_t);                                             \
     template hipError_t launch_pose_residual<T>(const T*, int64_t, const T*, int64_t, int64_t, int, T*, int64_t,    \
                                                 hipStream_t);
 KIN_STUBS(float)

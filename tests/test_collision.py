@@ -416,6 +416,59 @@ def test_gpu_attached_scene_specialized_equals_generic(dtype, with_base):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("with_base", [False, True])
+@pytest.mark.parametrize("scene_base", [True, False])
+def test_gpu_scene_constant_kernels_equal_generic(dtype, with_base, scene_base):
+    """kin_plan_specialize_scene (the union's groups, scene steps and boxes compiled in as well) == the generic
+    k_coll_scene bit for bit (torch.equal: up to the sign of a zero): distances, gradients, minimum and the
+    truncated distances, per-sample door angles and moved fridges and one state for the whole launch; a
+    fridge with and without its planar base.  A second AttachedUnionSDF of the same scene, not specialised,
+    runs the plan's other kernels with the same results."""
+    import kinhip
+    dev = torch.device("cuda", 0)
+    m, sscc, arm = _gpu_setup(with_base)
+    fr = kinhip.parse_urdf(golden("fridge.urdf"), with_base=scene_base)
+    sdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    other = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+    N = 3000
+    g = torch.Generator().manual_seed(13)
+    nq = 8 + (3 if with_base else 0)
+    Q = (torch.rand((nq, N), generator=g, dtype=torch.float64) * 2.4 - 1.2).to(dtype).to(dev)
+    cols = [torch.rand(N, generator=g, dtype=torch.float64) * 2.4]
+    if scene_base:
+        cols += [1.1 + 0.2 * torch.rand(N, generator=g, dtype=torch.float64),
+                 0.1 * torch.rand(N, generator=g, dtype=torch.float64) - 0.05,
+                 0.4 * torch.rand(N, generator=g, dtype=torch.float64) - 0.2]
+    else:  # (the fridge at the origin: move the arm's base into it instead)
+        if with_base:
+            Q[8] = (0.9 + 0.3 * torch.rand(N, generator=g, dtype=torch.float64)).to(dtype).to(dev)
+    SQ = torch.stack(cols).to(dtype).to(dev).contiguous()
+    gen = sscc.plan(arm, dtype=dtype)
+    spc = sscc.plan(arm, dtype=dtype).specialize().specialize_scene(sdf)
+    for sq in (SQ, SQ[:, 7].contiguous()):
+        for kw in (dict(dists=True, grads=True, min_dist=True), dict(dists=False, min_dist=True),
+                   dict(dists=True, grads=True, truncation=0.05)):
+            ref = gen.run(sdf, Q, scene_q=sq, **kw)
+            for si, sd in enumerate((sdf, other)):
+                for oi, (x, y) in enumerate(zip(ref, spc.run(sd, Q, scene_q=sq, **kw))):
+                    if x is None and y is None:
+                        continue
+                    bad = x != y
+                    if bool(bad.any()):
+                        idx = bad.nonzero()
+                        n0 = int(idx[0][-1])
+                        msg = (f"{kw} sdf {si} output {oi}: {int(bad.sum())} differ, max {float((x - y).abs().max()):.3e}; "
+                               f"first {idx[:6].tolist()} ref {x[bad][:6].tolist()} got {y[bad][:6].tolist()}; "
+                               f"sample {n0}: q {Q[:, n0].tolist()} scene {sq[:, n0].tolist() if sq.dim() == 2 else sq.tolist()}")
+                        if oi == 1:
+                            k = int(idx[0][0])
+                            msg += f"; sphere {k} row ref {x[k, :, n0].tolist()} got {y[k, :, n0].tolist()} d {ref[0][k, n0].item()}"
+                        assert False, msg
+    assert bool((ref[0] < 0.05).any())  # (the arm reaches the fridge in some samples)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("spec", [False, True])
 def test_gpu_collision_broad_phase_exact(dtype, spec):
     """Finite truncation enables the broad phase (spheres provably beyond truncation + the union's

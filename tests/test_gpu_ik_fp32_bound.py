@@ -88,3 +88,31 @@ def test_config4_answers_agree(setup, damp_err, max_step):
     er = np.arctan2(np.linalg.norm(vee, axis=0), 0.5 * (M[0, 0] + M[1, 1] + M[2, 2] - 1.0))
     print(f"fp32 answers checked in fp64: max |dp| {ep.max():.3e}, max |drot| {er.max():.3e} over {int(conv.sum())}")
     assert ep.max() <= 1e-3 + 5e-6 and er.max() <= 1e-3 + 5e-6, (float(ep.max()), float(er.max()))
+
+
+@pytest.mark.parametrize("lam", [0.0, 1e-3])
+def test_small_damping_keeps_the_fp64_solve(setup, lam):
+    """kin_ik_params accepts lambda = 0 and small lambdas, where the fp32 normal equations of a
+    near-singular arm lose the margin the fp32 solve relies on (lambda^2 = 1e-4 vs ~eps |J|^2).  Below lambda^2 =
+    0.99e-4 the fp32 kernel keeps the fp64 damped solve (KINHIP_IK_F32SOLVE_MIN_LAM2): from Fetch's singular
+    q = 0 (attempt 0) and random restarts, no NaN, and every target the fp32 kernel reports converged is a
+    solution when checked in fp64 (the oracle's FK), with a success rate within 1% of the fp64 oracle's."""
+    dev, plan, om, ids, gl, t32, tgt, N = setup
+    kw = dict(max_iters=64, restarts=3, tol_pos=1e-3, tol_rot=1e-3, lam=lam, seed=0, max_step=0.5)
+    Q, it, _ = plan.ik_dls(t32, torch.zeros((8, N), dtype=torch.float32, device=dev), **kw)
+    q = Q.double().cpu().numpy()
+    it = it.cpu().numpy()
+    assert np.isfinite(q).all()
+    _, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, **kw)
+    conv = it <= 64
+    print(f"lambda {lam}: fp32 kernel converged {conv.mean():.4f}, fp64 oracle {(rit <= 64).mean():.4f}")
+    assert conv.mean() >= (rit <= 64).mean() - 0.01
+    P = om.fk_batch(q[:, conv], ids, [gl.id])[0]
+    T = tgt[:, conv]
+    dp = np.linalg.norm(P[9:] - T[9:], axis=0)
+    assert (dp < 1e-3 + 5e-6).all(), float(dp.max())
+    for k in range(P.shape[1]):
+        Ta, Tt = np.eye(4), np.eye(4)
+        Ta[:3, :4] = P[:, k].reshape(4, 3).T
+        Tt[:3, :4] = T[:, k].reshape(4, 3).T
+        assert np.linalg.norm(O.rot_error(Tt, Ta)) < 1e-3 + 5e-6, k

@@ -26,6 +26,8 @@
 #   coll-dump                   the specialised collision source (A/B build, KINHIP_JIT_DUMP) for offline ISA
 #   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
 #   pr2-miss[=<n>]              tools/pr2_miss_study.py (PR2 collision-IK leg misses vs host SLSQP)
+#   scene-const                 door sweep A/B: scene tables as data vs compiled in (tools/scene_ab.py), x3 each,
+#                               plus a rocprofv3 kernel trace of both (VGPR counts)
 #   pts-probe                   tools/pts_probe (hipStreamPerThread after thread exit vs hipDeviceSynchronize)
 set -u -o pipefail
 mkdir -p gpurun_out/prof
@@ -65,6 +67,17 @@ for step in "$@"; do
       timeout -k 10 900 python tools/pr2_miss_study.py $n > gpurun_out/pr2_miss_study.json 2> gpurun_out/pr2_miss_study.err \
         || { tail -20 gpurun_out/pr2_miss_study.err; exit 11; }
       cut -c1-1500 gpurun_out/pr2_miss_study.json ;;
+    scene-const)
+      for r in 1 2 3; do
+        for c in 0 1; do
+          timeout -k 10 120 env SCENE_AB_CONST=$c python tools/scene_ab.py 15 2>&1 | quiet || exit 12
+        done
+      done
+      for c in 0 1; do
+        timeout -k 10 180 env SCENE_AB_CONST=$c rocprofv3 --kernel-trace --stats --output-format csv \
+          -d gpurun_out/prof/scene$c -o scene$c -- python3 tools/scene_ab.py 3 > gpurun_out/prof_scene$c.log 2>&1 \
+          || { tail -5 gpurun_out/prof_scene$c.log; exit 12; }
+      done ;;
     pts-probe)
       timeout -k 10 60 tools/pts_probe > gpurun_out/pts_probe.txt 2>&1; rc=$?; cat gpurun_out/pts_probe.txt
       [ $rc -eq 0 ] || exit 10 ;;

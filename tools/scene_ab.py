@@ -21,6 +21,8 @@ n = 1 << 20
 Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, seed=556, dtype=dt,
                            device=dev)
 asdf = kinhip.AttachedUnionSDF(fr, [fr.find_joint("door_joint")])
+if os.environ.get("SCENE_AB_CONST") == "1":  # kin_plan_specialize_scene: the fridge's tables compiled in too
+    cp.specialize_scene(asdf)
 g = torch.Generator().manual_seed(90)
 SQ = torch.zeros((4, n), dtype=torch.float64)
 SQ[0] = torch.rand(n, generator=g, dtype=torch.float64) * 2.4
@@ -55,5 +57,5 @@ for _ in range(blocks):
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1) / 20 * 1e3)
 chk = (float(r[0].double().abs().sum()), float(r[1].double().abs().sum()), float(r[2].double().sum()))
-print(f"scene median {statistics.median(ts):6.1f}us min {min(ts):6.1f}us max {max(ts):6.1f}us first {ts[0]:6.1f}us "
+print(f"{'const' if os.environ.get('SCENE_AB_CONST') == '1' else 'data '} scene median {statistics.median(ts):6.1f}us min {min(ts):6.1f}us max {max(ts):6.1f}us first {ts[0]:6.1f}us "
       f"chk {chk[0]:.9e} {chk[1]:.9e} {chk[2]:.9e}", flush=True)
