@@ -248,7 +248,11 @@ KINHIP_API int kin_get_jacobian_batch(kin_model* m, int32_t dtype, int32_t link_
  * tol_rot by the same iteration.                                                 */
 typedef struct kin_ik_params {
     int32_t max_iters;  /* e.g. 64 */
-    double lambda;      /* damping, e.g. 1e-2 */
+    double lambda;      /* damping, e.g. 1e-2.  0 is the undamped Gauss-Newton step: at a singular arm (Fetch at
+                           q = 0) its normal equations are singular and a target can end on NaN angles (iters =
+                           max_iters + 1), in fp64 as in the oracle.  The fp32 kernels solve the damped system in
+                           fp32 only for lambda^2 >= 0.99e-4 (and not in attempt 0's first 3 iterations), in fp64
+                           otherwise */
     double tol_pos;     /* |dp| tolerance, e.g. 1e-3 */
     double tol_rot;     /* |axis-angle error| tolerance, e.g. 1e-3 */
     double max_step;    /* max |dq|_inf per iteration, e.g. 0.5 */
@@ -272,13 +276,13 @@ typedef struct kin_ik_params {
                            round hands attempt 0 over after 5/8 of its iterations and phase 2 resumes it
                            beside the others, bit for bit).  The two-phase scratch (first call:
                            hipMalloc of 8 sets of ~16 MiB, 64 hand-over rings each, synchronising) is
-                           per plan: an eager call takes one of 4 sets and its stream waits on the device
-                           for the set's previous call (hipStreamWaitEvent) unless that call ran on the
-                           same stream, so calls from any thread, stream or handle (hipStreamPerThread
-                           included) never share a set in flight; the set its stream used last is
-                           preferred, else one that has finished, else the least recently used
-                           (kin_plan_ik_sched_stats counts the waits).  A captured graph keeps the set of
-                           its captured call. */
+                           per plan: an eager call takes one of 4 sets, ordered after the set's previous
+                           call by stream order (same stream) or, when that call is still in flight on
+                           another stream, by a host wait on its event, so calls from any thread, stream or
+                           handle (hipStreamPerThread included) never share a set in flight; the set its
+                           stream used last is preferred, else one that has finished, else the least
+                           recently used (kin_plan_ik_sched_stats counts the waits).  A captured graph
+                           keeps the set of its captured call. */
     int64_t index_base; /* global index of target 0 in the restart draws' hash: a caller that shards one
                            target set across processes passes its shard's offset, so every target gets
                            the same draws (and results) as in a single process; 0 otherwise */
@@ -316,11 +320,12 @@ KINHIP_API int kin_ik_dls_batch_trace(const kin_plan* p, const kin_ik_params* pr
  * diagnostics; no reference counterpart (the reference is single-threaded). */
 typedef struct kin_ik_sched_stats {
     uint64_t two_phase_calls;     /* eager calls that took a scratch set (two-phase schedule) */
-    uint64_t stream_waits;        /* of those, calls whose stream waited for another stream's call on the set */
-    uint64_t host_waits;          /* calls that found every set between take and event record in other
+    uint64_t set_waits;           /* of those, calls that waited on the host for the set's previous call, still
+                                     in flight on another stream (or another thread's per-thread stream) */
+    uint64_t busy_waits;          /* calls that found every set between take and event record in other
                                      threads and waited (microseconds) for one */
     uint64_t one_phase_fallbacks; /* eager two-phase calls that ran the one-phase schedule for want of a set
-                                     (0 by construction since ABI 2's hipStreamWaitEvent ordering) */
+                                     (0 by construction since round 6) */
     uint64_t captured_calls;      /* two-phase calls made inside a stream capture that took a graph set */
     uint64_t captured_one_phase;  /* captured two-phase calls that ran one phase (the 4 graph sets taken) */
 } kin_ik_sched_stats;

@@ -221,17 +221,16 @@ struct kin_plan {
     uint32_t jit_mask = 0;
     // two-phase IK schedule scratch (launch_ik_dls): allocated by the first kin_ik_dls_batch call that
     // runs the two-phase schedule.  An eager call takes an eager set (0..kIkEagerSets-1) and is ordered
-    // after the set's previous call ON THE DEVICE: unless that call ran on the same stream (one handle
-    // other than hipStreamPerThread names one stream for every thread, so stream order serialises the
-    // two), the call's stream waits for the set's event (hipStreamWaitEvent) before its launches.  No
-    // host-side guess about which stream or thread a set belongs to is needed, so any thread, stream or
-    // handle may take any set.  The choice only affects concurrency: the set this stream used last,
-    // else one whose last call has finished, else the least recently used one (the wait then costs at
-    // most the overlap with that older call).  ik_busy covers the host window between taking a set and
-    // recording its event; a call that finds all sets in that window waits for one (ik_cv).  A call
-    // made inside a stream capture takes one of the remaining sets for good (the captured graph replays
-    // with it, so it never meets an eager call or another graph), and once those are gone further
-    // captures run the one-phase schedule.
+    // after the set's previous call: by stream order when that call ran on the same stream (one handle
+    // other than hipStreamPerThread names one stream for every thread), else through the set's event --
+    // nothing to wait for once it has completed, otherwise a host wait (hipEventSynchronize; see
+    // ik_dls_batch for why not hipStreamWaitEvent).  No guess about which stream or thread a set belongs
+    // to is needed, so any thread, stream or handle may take any set.  The choice only affects
+    // concurrency: the set this stream used last, else one whose last call has finished, else the least
+    // recently used one.  ik_busy covers the host window between taking a set and recording its event; a
+    // call that finds all sets in that window waits for one (ik_cv).  A call made inside a stream capture
+    // takes one of the remaining sets for good (the captured graph replays with it, so it never meets an
+    // eager call or another graph), and once those are gone further captures run the one-phase schedule.
     static constexpr int kIkScratchSets = 8;
     static constexpr int kIkEagerSets = 4;
     static constexpr int64_t kIkScratchCap = int64_t(1) << 20;
@@ -2074,6 +2073,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
         const bool capturing = cs == hipStreamCaptureStatusActive;
         int set = -1;
+        hipEvent_t wait_ev = nullptr;  // the set's previous call ran on another stream: its event
         {
             std::unique_lock<std::mutex> lk(p->ik_mu);
             if (!p->d_ikscr) {
@@ -2112,18 +2112,16 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     waited = true;
                     p->ik_cv.wait(lk);
                 }
-                if (waited) ++p->ik_stats.host_waits;
+                if (waited) ++p->ik_stats.busy_waits;
                 hipError_t ee = hipSuccess;
                 if (!p->ik_ev[set]) {
                     ee = hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming);
                     if (ee != hipSuccess) p->ik_ev[set] = nullptr;
                 } else if (per_thread || p->ik_stream[set] != stream) {
-                    // device-side order after the set's previous call, whichever stream or thread made it
-                    ee = hipStreamWaitEvent((hipStream_t)stream, p->ik_ev[set], 0);
-                    ++p->ik_stats.stream_waits;
+                    wait_ev = p->ik_ev[set];  // (after the lock: see below)
                 }
                 if (ee != hipSuccess)
-                    return set_error(KIN_E_DEVICE, std::string("kin_ik_dls_batch: two-phase scratch ordering: ") +
+                    return set_error(KIN_E_DEVICE, std::string("kin_ik_dls_batch: two-phase scratch set: ") +
                                                        hipGetErrorString(ee));
                 p->ik_busy[set] = true;
                 p->ik_tick[set] = ++p->ik_ticks;
@@ -2136,6 +2134,28 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
             }
         }
         if (set >= 0 && !capturing) eager_set = set;
+        if (wait_ev) {
+            // Order this call after the set's previous call on another stream (or another thread's per-thread
+            // stream): nothing to do once that call has finished, else a host wait for it, outside the lock (the
+            // set is ours: ik_busy).  Not hipStreamWaitEvent: on this runtime, waiting on an event last recorded
+            // on a per-thread stream whose thread has since exited puts the waiting stream into a stream-capture
+            // state (its later events report hipErrorCapturedEvent, legacy-stream work fails "not permitted when
+            // capturing": tools/pts_probe.hip, profiles/r06_pts_probe.txt); the event itself stays valid for
+            // hipEventQuery / hipEventSynchronize, and a thread's exit drains its per-thread stream (same probe).
+            hipError_t ee = hipEventQuery(wait_ev);
+            if (ee == hipErrorNotReady) {
+                ee = hipEventSynchronize(wait_ev);
+                std::lock_guard<std::mutex> lk(p->ik_mu);
+                ++p->ik_stats.set_waits;
+            }
+            if (ee != hipSuccess) {
+                std::lock_guard<std::mutex> lk(p->ik_mu);
+                p->ik_busy[set] = false;
+                p->ik_cv.notify_one();
+                return set_error(KIN_E_DEVICE, std::string("kin_ik_dls_batch: two-phase scratch ordering: ") +
+                                                   hipGetErrorString(ee));
+            }
+        }
         if (set >= 0) {  // (no set left: one phase)
             unsigned char* base = (unsigned char*)p->d_ikscr + set_bytes * set;
             scr.fail_ctl = (uint32_t*)base;

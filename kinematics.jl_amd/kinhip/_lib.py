@@ -80,7 +80,7 @@ class IkParams(C.Structure):
 
 
 class IkSchedStats(C.Structure):
-    _fields_ = [("two_phase_calls", C.c_uint64), ("stream_waits", C.c_uint64), ("host_waits", C.c_uint64),
+    _fields_ = [("two_phase_calls", C.c_uint64), ("set_waits", C.c_uint64), ("busy_waits", C.c_uint64),
                 ("one_phase_fallbacks", C.c_uint64), ("captured_calls", C.c_uint64),
                 ("captured_one_phase", C.c_uint64)]
 

@@ -95,16 +95,24 @@ def test_small_damping_keeps_the_fp64_solve(setup, lam):
     """kin_ik_params accepts lambda = 0 and small lambdas, where the fp32 normal equations of a
     near-singular arm lose the margin the fp32 solve relies on (lambda^2 = 1e-4 vs ~eps |J|^2).  Below lambda^2 =
     0.99e-4 the fp32 kernel keeps the fp64 damped solve (KINHIP_IK_F32SOLVE_MIN_LAM2): from Fetch's singular
-    q = 0 (attempt 0) and random restarts, no NaN, and every target the fp32 kernel reports converged is a
-    solution when checked in fp64 (the oracle's FK), with a success rate within 1% of the fp64 oracle's."""
+    q = 0 (attempt 0) and random restarts, every target the fp32 kernel reports converged is a solution when
+    checked in fp64 (the oracle's FK), with a success rate within 1% of the fp64 oracle's.  Undamped (lambda = 0)
+    steps at a singular arm are undefined in either precision: the fp64 oracle too ends some targets on NaN
+    (3% at q = 0, include/kinhip.h); the kernel may not end more of them there than the oracle plus 1%, and
+    never reports one converged.  At lambda = 1e-3 every answer is finite."""
     dev, plan, om, ids, gl, t32, tgt, N = setup
     kw = dict(max_iters=64, restarts=3, tol_pos=1e-3, tol_rot=1e-3, lam=lam, seed=0, max_step=0.5)
     Q, it, _ = plan.ik_dls(t32, torch.zeros((8, N), dtype=torch.float32, device=dev), **kw)
     q = Q.double().cpu().numpy()
     it = it.cpu().numpy()
-    assert np.isfinite(q).all()
-    _, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, **kw)
+    rq, rit, _ = om.ik_dls_batch(np.zeros((8, N)), ids, gl.id, tgt, **kw)
+    nan32, nan64 = (~np.isfinite(q)).any(0), (~np.isfinite(rq)).any(0)
+    print(f"lambda {lam}: non-finite answers fp32 kernel {nan32.mean():.4f}, fp64 oracle {nan64.mean():.4f}")
+    assert nan32.mean() <= nan64.mean() + 0.01
+    if lam > 0:
+        assert not nan32.any()
     conv = it <= 64
+    assert not (conv & nan32).any()
     print(f"lambda {lam}: fp32 kernel converged {conv.mean():.4f}, fp64 oracle {(rit <= 64).mean():.4f}")
     assert conv.mean() >= (rit <= 64).mean() - 0.01
     P = om.fk_batch(q[:, conv], ids, [gl.id])[0]

@@ -1,13 +1,15 @@
 """Host threads on hipStreamPerThread (VERDICT r05 "next" 1).  The handle ((hipStream_t)2)
 names each calling thread's own default stream, so the two-phase IK's scratch sets (hand-over rings, fail
 lists) may be taken by calls on different streams.  Since round 6 every call that takes a set is ordered
-after the set's previous call on the device (hipStreamWaitEvent on the set's event, kinhip_host.cpp), so
-any number of threads, streams or handles share the 4 sets without ever running two calls in one set.
+after the set's previous call (stream order on the same stream, else a host wait on the set's event while
+that call is in flight; kinhip_host.cpp), so any number of threads, streams or handles share the 4 sets
+without ever running two calls in one set.
 
-Every result must equal the single-threaded reference bit for bit.  How a test may READ a worker's results
-follows the runtime rule tools/pts_probe.hip measured (profiles/r06_pts_probe.txt): hipDeviceSynchronize on
-the main thread does not wait for work an EXITED thread left on its per-thread stream, so a worker either
-synchronizes its stream before it ends or records an event there that the main thread waits on."""
+Every result must equal the single-threaded reference bit for bit, however the main thread reads them.
+tools/pts_probe.hip measured the runtime rule (profiles/r06_pts_probe.txt): a thread's exit blocks until its
+per-thread stream has drained, so after join() the results are complete -- the round-5 read (join, then a
+device-wide synchronize, nothing in the worker) was valid, and its failure was two calls sharing a scratch set
+(the cross-thread hipEventQuery reuse of that build), not an early read.  All three reads are asserted."""
 import ctypes as C
 import os
 import threading
@@ -58,8 +60,8 @@ def _run(config4, n_threads, streams, reps=6, sync="stream", concurrent=True):
     """n_threads workers, worker t on streams[t], reps IK calls each into its own outputs.
     sync: "stream" -- the worker synchronizes its stream before it ends;
           "event"  -- the worker only records an event on its stream, the main thread waits on it after join;
-          "device" -- nothing in the worker; the main thread's device-wide synchronize only (valid for
-                      streams that outlive the workers, i.e. not for per-thread streams: module doc).
+          "device" -- nothing in the worker; join and the main thread's device-wide synchronize only (the
+                      round-5 failing read; valid: module doc).
     concurrent=False runs the workers one after another (each joined before the next starts)."""
     dev, plan, tgt, Q0, ref_q, ref_it, N = config4
     prm = K.IkParams(64, 1e-2, 1e-3, 1e-3, 0.5, 1, 3, 0, 0, 0, 0.0)
@@ -120,11 +122,11 @@ def test_controls_one_thread_and_own_streams(config4):
     assert _clean(own), own
 
 
-@pytest.mark.parametrize("sync", ["stream", "event"])
+@pytest.mark.parametrize("sync", ["device", "stream", "event"])
 def test_two_threads_on_the_per_thread_stream_handle(config4, sync,
                                                       reps=int(os.environ.get("STREAMS_REPS", "6"))):
     """The round-5 failing configuration (two threads, per-thread handle, 6 back-to-back two-phase calls
-    each, no synchronize in the worker's loop), read in either of the two ways the runtime allows."""
+    each, no synchronize in the worker; sync="device" is its exact read), and the other two reads."""
     plan = config4[1]
     before = plan.ik_sched_stats()
     got = _run(config4, 2, [HIP_STREAM_PER_THREAD, HIP_STREAM_PER_THREAD], reps, sync=sync)
@@ -138,7 +140,7 @@ def test_two_threads_on_the_per_thread_stream_handle(config4, sync,
 
 def test_more_threads_than_scratch_sets_concurrently(config4):
     """6 threads at once on the per-thread handle (more than the 4 sets): sets are shared in turn, each
-    call ordered after the set's previous one on the device; no call runs the one-phase schedule."""
+    call ordered after the set's previous one; no call runs the one-phase schedule."""
     plan = config4[1]
     before = plan.ik_sched_stats()
     got = _run(config4, 6, [HIP_STREAM_PER_THREAD] * 6, reps=3, sync="event")
@@ -146,7 +148,6 @@ def test_more_threads_than_scratch_sets_concurrently(config4):
     assert _clean(got), got
     assert after["one_phase_fallbacks"] == 0
     assert after["two_phase_calls"] - before["two_phase_calls"] == 18
-    assert after["stream_waits"] > before["stream_waits"]
 
 
 def test_exited_threads_leave_no_sets_behind(config4):

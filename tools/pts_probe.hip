@@ -6,12 +6,18 @@
 // hipStreamPerThread and records an event there, then either exits at once or stays alive until the
 // main thread is done.  The main thread joins (or not), calls hipDeviceSynchronize() and reads the flag
 // through a non-blocking stream (no implicit null-stream ordering), then waits on the event and reads
-// again.  Build: hipcc --offload-arch=gfx950 -O2 -o pts_probe tools/pts_probe.hip
+// again.
+// Second question (round 6, from a failing test): may another thread order its own per-thread stream after
+// that event with hipStreamWaitEvent once the recording thread has exited (its per-thread stream destroyed)?
+// The waiting thread checks hipStreamIsCapturing on its stream and records / synchronizes an event of its own;
+// the host-side alternative (hipEventQuery, hipEventSynchronize on the old event) is run beside it.
+// Build: hipcc --offload-arch=gfx950 -O2 -o pts_probe tools/pts_probe.hip
 #include <hip/hip_runtime.h>
 
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <thread>
 
 __global__ void spin_then_flag(int* flag, unsigned long long ticks) {
@@ -80,6 +86,41 @@ static int trial(bool exit_before_sync, int* flag, hipStream_t rd, unsigned long
     return 0;
 }
 
+static int wait_after_exit(bool device_wait, int* flag, unsigned long long ticks) {
+    hipEvent_t ev;
+    CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    std::thread a([&] {
+        (void)hipSetDevice(0);
+        hipLaunchKernelGGL(spin_then_flag, dim3(1), dim3(1), 0, hipStreamPerThread, flag, ticks / 30);
+        (void)hipEventRecord(ev, hipStreamPerThread);
+    });
+    a.join();  // (its per-thread stream drained and destroyed at exit: see the first question)
+    int r_wait = -1, r_cap = -1, r_rec = -1, r_sync = -1, r_q = -1;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    std::thread b([&] {
+        (void)hipSetDevice(0);
+        hipEvent_t mine;
+        (void)hipEventCreateWithFlags(&mine, hipEventDisableTiming);
+        if (device_wait) {
+            r_wait = (int)hipStreamWaitEvent(hipStreamPerThread, ev, 0);
+        } else {
+            r_q = (int)hipEventQuery(ev);
+            r_wait = (int)hipEventSynchronize(ev);
+        }
+        r_cap = (int)hipStreamIsCapturing(hipStreamPerThread, &cs);
+        r_rec = (int)hipEventRecord(mine, hipStreamPerThread);
+        r_sync = (int)hipEventSynchronize(mine);
+        (void)hipStreamSynchronize(hipStreamPerThread);
+        (void)hipEventDestroy(mine);
+    });
+    b.join();
+    std::printf("%-44s wait %d, hipStreamIsCapturing %d (status %d), own event record %d, its synchronize %d%s\n",
+                device_wait ? "other thread, hipStreamWaitEvent:" : "other thread, hipEventQuery + Synchronize:", r_wait,
+                r_cap, (int)cs, r_rec, r_sync, device_wait ? "" : (" (query " + std::to_string(r_q) + ")").c_str());
+    CK(hipEventDestroy(ev));
+    return 0;
+}
+
 int main() {
     CK(hipSetDevice(0));
     int* flag = nullptr;
@@ -94,6 +135,10 @@ int main() {
     for (int rep = 0; rep < 3; ++rep) {
         if (trial(false, flag, rd, ticks)) return 1;
         if (trial(true, flag, rd, ticks)) return 1;
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+        if (wait_after_exit(false, flag, ticks)) return 1;
+        if (wait_after_exit(true, flag, ticks)) return 1;
     }
     CK(hipStreamDestroy(rd));
     CK(hipFree(flag));
