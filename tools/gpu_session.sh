@@ -9,6 +9,7 @@
 #                               the bench compiles) + tools/isa_check.py over them and the generic kernels
 #   smoke                       __graft_entry__.smoke()
 #   bench                       python bench.py -> gpurun_out/bench.json
+#   bench-driver                the driver's command (--gpus 1 --steps 20 --warmup 5) -> gpurun_out/bench_driver.json
 #   bench-trace                 rocprofv3 --kernel-trace --stats of `bench.py --no-cpu` (gpurun_out/prof/bench)
 #   sweep                       python bench.py --no-cpu --sweep -> gpurun_out/bench_sweep.json
 #   rccl                        the RCCL test + the bench under a one-rank RCCL group (KINHIP_DIST_ALWAYS_GROUP=1)
@@ -86,6 +87,10 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 3; }
       cut -c1-400 gpurun_out/bench.json ;;
+    bench-driver)
+      timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.json \
+        2> gpurun_out/bench_driver.err || { tail gpurun_out/bench_driver.err; exit 3; }
+      cut -c1-300 gpurun_out/bench_driver.json ;;
     bench-trace)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/bench -o bench -- \
         python3 bench.py --no-cpu > gpurun_out/bench_rocprof.log 2>&1 || { tail gpurun_out/bench_rocprof.log; exit 4; } ;;

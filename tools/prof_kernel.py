@@ -79,6 +79,7 @@ elif a.what == "scene32":  # bench f2_scene_door_sweep: boxes attached to the fr
     cp = sscc.plan(arm, dtype=dt)
     if SPEC:
         cp.specialize()
+        cp.specialize_scene(asdf)  # (as the bench's leg: the fridge's tables compiled in, kinhip_jit_collc_1)
     g = torch.Generator().manual_seed(90)
     SQ = torch.zeros((4, a.n), dtype=torch.float64)
     SQ[0] = torch.rand(a.n, generator=g, dtype=torch.float64) * 2.4
