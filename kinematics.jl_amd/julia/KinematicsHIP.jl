@@ -26,6 +26,7 @@
 module KinematicsHIP
 
 using Kinematics
+using Kinematics: Joint  # (not in Kinematics.jl's export list, src/Kinematics.jl:45-73)
 using AMDGPU
 
 const libkinhip = joinpath(@__DIR__, "..", "lib", "libkinhip.so")

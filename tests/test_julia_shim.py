@@ -166,3 +166,40 @@ def test_every_cached_plan_path_goes_through_the_staleness_check():
             continue
         for body in bodies:
             assert "hm.plans" not in body and "x.plans" not in body, name
+
+
+# Kinematics.jl's export list (src/Kinematics.jl:45-73, the names a `using Kinematics` brings in)
+KINEMATICS_EXPORTS = {
+    "Transform", "rotation", "translation", "rpy", "CacheVector", "invalidate_cache!", "set_cache!", "iscached",
+    "get_cache", "extend!", "PseudoStack", "parse_urdf", "Mechanism", "parent_link", "child_link", "child_links",
+    "parent_joint", "child_joints", "find_link", "find_joint", "isroot", "isleaf", "joint_angle", "set_joint_angle",
+    "set_joint_angles", "is_relevant", "get_joint_angles!", "get_joint_angles", "add_new_link", "User", "Link",
+    "get_transform", "get_jacobian", "get_jacobian!", "BoxSDF", "UnionSDF", "SweptSphereCollisionChecker",
+    "collision_trimesh", "compute_swept_sphere", "add_coll_links", "add_sscc", "compute_coll_dists",
+    "compute_coll_dists!", "compute_coll_dists_and_grads!", "compute_coll_dists_and_grads", "add_mechanism", "update",
+    "add_frame", "to_affine_map", "create_vis_sphere", "add_sdf", "MechanismVisualizer", "create_straight_trajectory",
+    "plan_trajectory", "PoseConstraint", "ConfigurationConstraint", "inverse_kinematics!", "load_pr2", "rarm_joints",
+    "larm_joints", "rarm_collision_links", "larm_collision_links", "reset_manip_pose", "__skrobot__"}
+JULIA_BUILTIN_TYPES = {"Vector", "Ptr", "Int32", "Int64", "Int", "UInt32", "UInt64", "Float32", "Float64", "Bool", "Union",
+                       "Type", "Integer", "Real", "Dict", "Cint", "Cvoid", "Cstring", "Ref", "Nothing", "Any", "Tuple",
+                       "Array", "Matrix", "SubArray", "AbstractMatrix", "AbstractArray", "AbstractVector", "Symbol"}
+
+
+def test_type_names_in_signatures_resolve():
+    """Every type name the shim uses in a signature (`x::T`, `Vector{<:T}`) resolves in the module: a
+    Julia builtin, an AMDGPU array type, a name the shim defines or imports (`using Kinematics: X`), one of
+    Kinematics.jl's exports, or a qualified `Kinematics.X`.  (Round 6: `Joint` is not exported; the shim
+    used it unqualified in every batched signature since round 1, an UndefVarError at load.)"""
+    src = open(SHIM).read()
+    code = "\n".join(line.split("#", 1)[0] for line in src.splitlines())
+    defined = set(re.findall(r"^(?:mutable\s+)?struct\s+(\w+)", code, flags=re.M))
+    defined |= set(re.findall(r"^const\s+(\w+)", code, flags=re.M))
+    imported = set()
+    for m in re.finditer(r"^using\s+Kinematics:\s*(.+)$", code, flags=re.M):
+        imported |= {x.strip() for x in m.group(1).split(",")}
+    amdgpu = {"ROCArray", "ROCMatrix", "ROCVector"}
+    used = {n.rstrip(".") for n in re.findall(r"(?:::|<:)\s*([A-Za-z_][\w.]*)", code)}  # (`Integer...` varargs)
+    bad = sorted(n for n in used
+                 if not n.startswith(("Kinematics.", "AMDGPU."))
+                 and n not in JULIA_BUILTIN_TYPES | amdgpu | defined | imported | KINEMATICS_EXPORTS)
+    assert not bad, bad

@@ -49,9 +49,10 @@ WORK = {  # workload -> (kernel substring, algorithmic bytes per launch, note)
                 "config 5 validity: FK + 14 spheres vs 7-box fridge SDF, min distance, fp32, N = 2^20, specialised"),
     "collg32s": ("kinhip_jit_coll_1_f32", (8 + 14 + 14 * 8) * 4 * (1 << 20),
                  "config 5 / IneqConst: 14 distances + 14x8 gradients, fp32, N = 2^20, specialised"),
-    "scene32s": ("kinhip_jit_colls_1_2_f32", ((8 + 4) + 14 + 14 * 8 + 1) * 4 * (1 << 20),
+    "scene32s": ("kinhip_jit_collc_1_f32", ((8 + 4) + 14 + 14 * 8 + 1) * 4 * (1 << 20),
                  "f2 door sweep (bench f2_scene_door_sweep): boxes attached to the fridge, one door angle per sample, "
-                 "14 distances + 14x8 gradients + the minimum, fp32, N = 2^20, specialised 2-group scene kernel"),
+                 "14 distances + 14x8 gradients + the minimum, fp32, N = 2^20, scene-specialised kernel (round 6: "
+                 "kin_plan_specialize_scene, the fridge's tables compiled in; rounds 3-5: kinhip_jit_colls_1_2)"),
     "cik32s": ("kinhip_jit_ikt_6_", 4096 * (12 + 8 + 8 + 1 + 3) * 4,
                "f3 stage 2 (bench f3_collision_ik): kin_ik_coll_batch of 4,096 fridge targets from stage 1's answers, "
                "128 iterations, 3 restarts side by side in 4 lane groups of 16 sphere lanes, fp32, specialised"),
