@@ -467,6 +467,18 @@ KINHIP_API int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, co
                                        const kin_ik_coll_params* cprm, const void* target, int64_t ldt,
                                        const void* scene_q, int64_t lds, const void* q0, void* q, int64_t ldq,
                                        int64_t n, int32_t* iters, void* err, int64_t lde, void* stream);
+/* kin_ik_coll_batch (a static kin_sdf: scene_q / lds ignored) or kin_ik_coll_batch_scene (an attached one)
+ * with a restart origin q_alt ([n_q(+3)][ldq], the layout of q; may alias q0 or q): attempt 0 starts
+ * from q0; restart attempt 1 takes the free joint variables from q_alt instead of a seeded draw, and
+ * every restart (1, 2, ...) takes its base columns from q_alt instead of q0; attempts >= 2 draw the
+ * joints as before.  For the bistage solve (src/inverse_kinematics.jl:1-21): stage 2 starts from
+ * stage 1's answer, whose base stage 1 has moved; with q_alt = the pose stage 1 started from, the
+ * restarts leave that basin (PR2 fridge leg: DESIGN.md §4.6).  q_alt = NULL: exactly
+ * kin_ik_coll_batch(_scene). */
+KINHIP_API int kin_ik_coll_batch_alt(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
+                                     const kin_ik_coll_params* cprm, const void* target, int64_t ldt,
+                                     const void* scene_q, int64_t lds, const void* q0, const void* q_alt, void* q,
+                                     int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Planning constraints over waypoints (src/planning.jl) */

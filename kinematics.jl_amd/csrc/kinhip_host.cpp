@@ -1808,8 +1808,9 @@ int kin_coll_ik_plan_create(const kin_model* m, const kin_coll_desc* c, int32_t 
 
 namespace {
 int ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
-                  const void* target, int64_t ldt, const void* scene_q, int64_t lds, bool scene, const void* q0, void* q,
-                  int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream, const char* fn) {
+                  const void* target, int64_t ldt, const void* scene_q, int64_t lds, bool scene, const void* q0,
+                  const void* q_alt, void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream,
+                  const char* fn) {
     auto bad = [&](int code, const std::string& w) { return set_error(code, std::string(fn) + ": " + w); };
     if (!p || !sdf || !prm || !cp) return bad(KIN_E_INVALID, "null argument");
     if (!p->is_coll_ik) return bad(KIN_E_INVALID, "plan was not made by kin_coll_ik_plan_create");
@@ -1830,8 +1831,9 @@ int ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* pr
     if (prm->lanes != 0 && prm->lanes != 1 && prm->lanes != 2 && prm->lanes != 4 && prm->lanes != 8 &&
         prm->lanes != 16 && prm->lanes != 64)
         return bad(KIN_E_INVALID, "kin_ik_params.lanes must be 0 (auto), 1, 2, 4, 8, 16 or 64");
-    const IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
-                   prm->restarts, prm->seed, prm->lanes, prm->index_base, 0.0};
+    IkArgs a{prm->max_iters, prm->lambda, prm->tol_pos, prm->tol_rot, prm->max_step, prm->with_rot,
+             prm->restarts, prm->seed, prm->lanes, prm->index_base, 0.0};
+    a.q_alt = q_alt;
     const IkcArgs c{cp->margin, cp->band, cp->weight, cp->feas};
     const CollArgs ca{INFINITY, 0.0, sdf->n_boxes, sdf->n_aabb, 0, 0, {sdf->bc[0], sdf->bc[1], sdf->bc[2]},
                       {sdf->bh[0], sdf->bh[1], sdf->bh[2]}};
@@ -1861,16 +1863,24 @@ int ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* pr
 int kin_ik_coll_batch(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm, const kin_ik_coll_params* cp,
                       const void* target, int64_t ldt, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters,
                       void* err, int64_t lde, void* stream) {
-    return ik_coll_batch(p, sdf, prm, cp, target, ldt, nullptr, 0, false, q0, q, ldq, n, iters, err, lde, stream,
-                         "kin_ik_coll_batch");
+    return ik_coll_batch(p, sdf, prm, cp, target, ldt, nullptr, 0, false, q0, nullptr, q, ldq, n, iters, err, lde,
+                         stream, "kin_ik_coll_batch");
 }
 
 int kin_ik_coll_batch_scene(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
                             const kin_ik_coll_params* cp, const void* target, int64_t ldt, const void* scene_q,
                             int64_t lds, const void* q0, void* q, int64_t ldq, int64_t n, int32_t* iters, void* err,
                             int64_t lde, void* stream) {
-    return ik_coll_batch(p, sdf, prm, cp, target, ldt, scene_q, lds, true, q0, q, ldq, n, iters, err, lde, stream,
-                         "kin_ik_coll_batch_scene");
+    return ik_coll_batch(p, sdf, prm, cp, target, ldt, scene_q, lds, true, q0, nullptr, q, ldq, n, iters, err, lde,
+                         stream, "kin_ik_coll_batch_scene");
+}
+
+int kin_ik_coll_batch_alt(const kin_plan* p, const kin_sdf* sdf, const kin_ik_params* prm,
+                          const kin_ik_coll_params* cp, const void* target, int64_t ldt, const void* scene_q,
+                          int64_t lds, const void* q0, const void* q_alt, void* q, int64_t ldq, int64_t n,
+                          int32_t* iters, void* err, int64_t lde, void* stream) {
+    return ik_coll_batch(p, sdf, prm, cp, target, ldt, scene_q, lds, sdf && sdf->attached, q0, q_alt, q, ldq, n,
+                         iters, err, lde, stream, "kin_ik_coll_batch_alt");
 }
 
 namespace {

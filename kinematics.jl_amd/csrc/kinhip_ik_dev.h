@@ -236,6 +236,9 @@ struct IkArgsT {
     // [trace_ld]), or null
     T* trace;
     int64_t trace_ld;
+    // k_ik_tree (kin_ik_coll_batch_alt): the restart origin -- attempt 1's free variables, every restart's base --
+    // or null
+    const T* q_alt;
 };
 
 // lambda^2 + mu (ep^2 + er^2) rounded operation by operation, as the oracle forms it (no contraction)

@@ -78,6 +78,7 @@ hipError_t launch_ik_tree(const KIkcProg<T>& P, const KIkcStep<T>* steps, const 
         const int64_t cn = std::min(kIkChunk, n - s0);
         at.ibase = a.index_base + s0;
         at.q0 = q0 ? q0 + s0 : nullptr;
+        at.q_alt = a.q_alt ? (const T*)a.q_alt + s0 : nullptr;
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;

@@ -291,7 +291,8 @@ __device__ __forceinline__ T attempt_min_t(T v) {
 
 // starting angles of an attempt: attempt 0 from q0; attempt k >= 1 re-draws every free joint variable
 // within its limits (U[-pi, pi] if unbounded) from the counter hash of k_ik_dls (ik_seed_u01), other
-// variables from q0 (the base is reset by the caller)
+// variables from q0 (the base: the caller).  With a second start pose (a.q_alt, kin_ik_coll_batch_alt) attempt 1
+// takes its free joint variables from q_alt instead of a draw (and every restart its base from q_alt).
 template <typename T, int MAXV>
 __device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>& a, const T* __restrict__ q,
                                           int64_t ldq, uint32_t off, int64_t gi, int att, T (&qs)[MAXV]) {
@@ -301,7 +302,9 @@ __device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>
             qs[v] = T(0);
             continue;
         }
-        if (att > 0 && ((P.free_mask & P.joint_mask) >> v) & 1u) {
+        if (att == 1 && a.q_alt && ((P.free_mask & P.joint_mask) >> v) & 1u) {
+            qs[v] = ld_soa(a.q_alt, v, ldq, off);
+        } else if (att > 0 && ((P.free_mask & P.joint_mask) >> v) & 1u) {
             double lo = (double)P.vlo[v], hi = (double)P.vhi[v];
             if (!isfinite(lo) || !isfinite(hi)) { lo = -3.14159265358979323846; hi = 3.14159265358979323846; }
             qs[v] = (T)(lo + (hi - lo) * ik_seed_u01(a.seed, gi, att, v));
@@ -381,12 +384,16 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
     constexpr int MG = MAXG > 0 ? MAXG : 1;
     SceneCtx<T, MG> sc;
     if constexpr (MAXG > 0) scene_frames(sc, sa, off);
-    T b0[3] = {T(0), T(0), T(0)};
+    // the base of an attempt: q0's; with q_alt every restart's (k >= 1) from q_alt
+    T b0[3] = {T(0), T(0), T(0)}, b1[3] = {T(0), T(0), T(0)};
     if (base)
-        for (int k = 0; k < 3; ++k) b0[k] = ld_soa(qin, P.base_col + k, ldq, off);
-    T qs[MAXV], b[3] = {b0[0], b0[1], b0[2]};
+        for (int k = 0; k < 3; ++k) {
+            b0[k] = ld_soa(qin, P.base_col + k, ldq, off);
+            b1[k] = a.q_alt ? ld_soa(a.q_alt, P.base_col + k, ldq, off) : b0[k];
+        }
     const int L = a.attempt_len;
     int att = ga, it = ga > 0 ? ga * L + 1 : 0;  // attempt 0 from q0 at iteration 0, k >= 1 re-drawn at kL + 1
+    T qs[MAXV], b[3] = {att > 0 ? b1[0] : b0[0], att > 0 ? b1[1] : b0[1], att > 0 ? b1[2] : b0[2]};
     ikt_start<T, MAXV>(P, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
     uint32_t held = 0;  // bit v: variable v held out of the step
     bool conv = false;
@@ -649,7 +656,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             }
             it = att * L + 1;
             ikt_start<T, MAXV>(P, a, qin, ldq, off, a.ibase + (int64_t)gi, att, qs);
-            b[0] = b0[0]; b[1] = b0[1]; b[2] = b0[2];
+            for (int k = 0; k < 3; ++k) b[k] = b1[k];  // (att >= 1 here)
             held = 0;
             continue;
         }

@@ -84,6 +84,7 @@ struct IkArgs {
     double damp_err;     // error-scaled damping (k_ik_dls only)
     void* trace = nullptr;  // kin_ik_dls_batch_trace: [2 (max_iters + 1)][trace_ld] residual norms per iterate
     int64_t trace_ld = 0;
+    const void* q_alt = nullptr;  // kin_ik_coll_batch_alt: attempt 1's start pose (same layout as q), or null
 };
 
 // restart schedule of kin_ik_params: attempt length L (0: no restarts) and the attempts it reaches

@@ -483,9 +483,10 @@ end
 """Batched collision-aware IK, inverse_kinematics!(m, link, joints, target, sscc, sdf; use_bistage)
 (src/inverse_kinematics.jl:1-21) for every row of `targets` (N, 12): stage 1 the collision-free DLS
 (kin_ik_dls_batch_from, seeds Q0), stage 2 the IneqConst(sscc, joints, sdf, 1, margin) sphere rows, both on
-one plan of kin_coll_ik_plan_create.  A static `HIPSDF(UnionSDF)` runs kin_ik_coll_batch; an attached one
+one plan of kin_coll_ik_plan_create, stage 2's restart attempt 1 from Q0 (kin_ik_coll_batch_alt).  A static
+`HIPSDF(UnionSDF)` runs kin_ik_coll_batch's kernel; an attached one
 (`HIPSDF(fridge, [door_joint])`, the reference's `UnionSDF(fridge)` of test/test_inverse_kinematics.jl:55
-and fridge_demo.jl) runs kin_ik_coll_batch_scene with `scene_q`: the scene columns per target, an
+and fridge_demo.jl) runs kin_ik_coll_batch_scene's kernel with `scene_q`: the scene columns per target, an
 (N, n_scene_cols) ROCMatrix (e.g. a door angle per target), or one ROCVector for the whole batch.
 Returns (Q, iters, err (N, 3))."""
 function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, targets::ROCMatrix{T},
@@ -513,20 +514,16 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
         copyto!(Q1, Q0)
     end
     cprm = KinIkCollParams(margin, band, weight, feas)
-    if sdf.attached
-        lds = scene_q isa ROCMatrix ? stride(scene_q, 2) : 0  # (N, cols) per target, or one vector
-        check(ccall((:kin_ik_coll_batch_scene, libkinhip), Cint,
-                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Int64,
-                     Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),
-                    p, sdf.handle, prm, cprm, pointer(targets), stride(targets, 2), pointer(scene_q), lds,
-                    pointer(Q1), pointer(Q), stride(Q, 2), N, pointer(iters), pointer(err), N, stream_ptr()))
-        return Q, iters, err
-    end
-    check(ccall((:kin_ik_coll_batch, libkinhip), Cint,
-                (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Ptr{T}, Int64,
-                 Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),
-                p, sdf.handle, prm, cprm, pointer(targets), stride(targets, 2), pointer(Q1), pointer(Q), stride(Q, 2),
-                N, pointer(iters), pointer(err), N, stream_ptr()))
+    # stage 2 from stage 1's answers; its restart attempt 1 from Q0, the pose stage 1 started from
+    # (kin_ik_coll_batch_alt; static or attached union alike)
+    sq = sdf.attached ? pointer(scene_q) : Ptr{T}(C_NULL)
+    lds = scene_q isa ROCMatrix ? stride(scene_q, 2) : 0  # (N, cols) per target, or one vector
+    check(ccall((:kin_ik_coll_batch_alt, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{T}, Int64, Ptr{T}, Int64,
+                 Ptr{T}, Ptr{T}, Ptr{T}, Int64, Int64, Ptr{Int32}, Ptr{T}, Int64, Ptr{Cvoid}),
+                p, sdf.handle, prm, cprm, pointer(targets), stride(targets, 2), sq, lds, pointer(Q1),
+                use_bistage ? pointer(Q0) : Ptr{T}(C_NULL), pointer(Q), stride(Q, 2), N, pointer(iters),
+                pointer(err), N, stream_ptr()))
     Q, iters, err
 end
 
@@ -591,7 +588,8 @@ end
 call above (it moves the mechanism to its answer, as the reference's NLopt stage 1 does through
 f_objective's set_joint_angles); stage 2 solves the same objective subject to IneqConst(sscc, joints, sdf, 1,
 margin)'s sphere distances (:16-17) and the joint limits from the mechanism's current angles: the batched
-kin_ik_coll_batch kernel on a batch of one, 3 seeded restarts, converged when |dp|, |d rpy| < 1e-6 with every
+kin_ik_coll_batch kernel on a batch of one, 3 restarts (with use_bistage the first from the angles stage 1
+started from, kin_ik_coll_batch_alt; the others seeded draws), converged when |dp|, |d rpy| < 1e-6 with every
 sphere at >= margin - 1e-6 (:FTOL_REACHED); otherwise the attempt of lowest merit, :MAXEVAL_REACHED.  `sdf`
 is the reference's UnionSDF / BoxSDF (a snapshot at the scene's current angles, HIPSDF(sdf)) or a HIPSDF; an
 attached HIPSDF(scene, joints) takes `scene_q`, its scene column values (a ROCVector).  A checker without
@@ -604,6 +602,7 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
                                         scene_q=nothing)
     m = hm.m
     m === sscc.mech || throw(ArgumentError("the HIPModel must be the checker's mechanism (sscc.mech)"))
+    q_start = angles_batch(m, joints)  # stage 2's restart attempt 1 starts here (kin_ik_coll_batch_alt)
     if use_bistage  # stage 1 seeds stage 2 (src/inverse_kinematics.jl:8-13)
         Kinematics.inverse_kinematics!(hm, link, joints, target_pose; ftol=ftol, with_rot=with_rot,
                                        max_iters=max_iters, lambda=lambda, max_step=max_step)
@@ -618,19 +617,13 @@ function Kinematics.inverse_kinematics!(hm::HIPModel, link::Link, joints::Vector
     err = ROCMatrix{Float64}(undef, 1, 3)
     prm = KinIkParams(max_iters, lambda, 1e-6, 1e-6, max_step, with_rot ? Int32(2) : Int32(0), 3, 0, 0, 0, 0.0)
     cprm = KinIkCollParams(margin, 0.0, 1.0, 1e-6)
-    if hs.attached
-        check(ccall((:kin_ik_coll_batch_scene, libkinhip), Cint,
-                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{Float64}, Int64, Ptr{Float64},
-                     Int64, Ptr{Float64}, Ptr{Float64}, Int64, Int64, Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
-                    p, hs.handle, prm, cprm, pointer(tgt), 1, pointer(scene_q), 0, pointer(q0), pointer(q), 1, 1,
-                    pointer(iters), pointer(err), 1, stream_ptr()))
-    else
-        check(ccall((:kin_ik_coll_batch, libkinhip), Cint,
-                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{Float64}, Int64, Ptr{Float64},
-                     Ptr{Float64}, Int64, Int64, Ptr{Int32}, Ptr{Float64}, Int64, Ptr{Cvoid}),
-                    p, hs.handle, prm, cprm, pointer(tgt), 1, pointer(q0), pointer(q), 1, 1, pointer(iters),
-                    pointer(err), 1, stream_ptr()))
-    end
+    check(ccall((:kin_ik_coll_batch_alt, libkinhip), Cint,
+                (Ptr{Cvoid}, Ptr{Cvoid}, Ref{KinIkParams}, Ref{KinIkCollParams}, Ptr{Float64}, Int64, Ptr{Float64},
+                 Int64, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Int64, Ptr{Int32}, Ptr{Float64}, Int64,
+                 Ptr{Cvoid}),
+                p, hs.handle, prm, cprm, pointer(tgt), 1, hs.attached ? pointer(scene_q) : Ptr{Float64}(C_NULL), 0,
+                pointer(q0), use_bistage ? pointer(q_start) : Ptr{Float64}(C_NULL), pointer(q), 1, 1,
+                pointer(iters), pointer(err), 1, stream_ptr()))
     qv = vec(Array(q))
     set_joint_angles(m, joints, qv)
     qv, (Array(iters)[1] <= max_iters ? :FTOL_REACHED : :MAXEVAL_REACHED)

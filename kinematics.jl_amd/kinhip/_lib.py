@@ -41,7 +41,7 @@ EXPORTS = [
     "kin_sdf_create_boxes", "kin_sdf_destroy", "kin_coll_plan_create", "kin_coll_batch",
     "kin_ineq_const_batch", "kin_pose_const_batch",
     "kin_coll_ik_plan_create", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_sdf_create_attached",
-    "kin_coll_batch_scene", "kin_plan_ik_sched_stats", "kin_plan_specialize_scene",
+    "kin_coll_batch_scene", "kin_plan_ik_sched_stats", "kin_plan_specialize_scene", "kin_ik_coll_batch_alt",
 ]
 
 
@@ -146,6 +146,7 @@ def lib():
         "kin_coll_batch_scene": ([P, P, C.c_double, P, I64, P, I64, I64, P, I64, P, I64, P, P], C.c_int),
         "kin_ik_coll_batch": ([P, P, P, P, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_ik_coll_batch_scene": ([P, P, P, P, P, I64, P, I64, P, P, I64, I64, P, P, I64, P], C.c_int),
+        "kin_ik_coll_batch_alt": ([P, P, P, P, P, I64, P, I64, P, P, P, I64, I64, P, P, I64, P], C.c_int),
         "kin_plan_ik_sched_stats": ([P, P], C.c_int),
         "kin_plan_specialize_scene": ([P, P], C.c_int),
     }

@@ -278,19 +278,22 @@ class CollisionIKPlan(Plan):
     def ik_coll(self, sdf, targets: torch.Tensor, Q: torch.Tensor, Q0: Optional[torch.Tensor] = None,
                 margin=0.02, band=0.0, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
                 max_step=0.5, with_rot=2, restarts=0, seed=0, lanes=0, index_base=0, stream=None,
-                scene_q: Optional[torch.Tensor] = None):
+                scene_q: Optional[torch.Tensor] = None, Q_alt: Optional[torch.Tensor] = None):
         """Stage 2 alone (kin_ik_coll_batch): from Q0 (or Q in place) -> (Q, iters [N], err [3, N]:
         |dp|, |rot|, min sphere distance).  iters > max_iters: not converged (Q, err: the attempt with the
         best end state).  `lanes`: 0 = auto (restart attempts side by side and spheres shared out over lanes
         for small batches), 1 = attempts in sequence on one lane; the results do not depend on it.
         With an ``AttachedUnionSDF`` (kin_ik_coll_batch_scene): `scene_q` = its scene columns per target
-        (n_scene_cols, N) or one vector (n_scene_cols,) for the batch."""
+        (n_scene_cols, N) or one vector (n_scene_cols,) for the batch.  `Q_alt` (Q's shape and strides;
+        kin_ik_coll_batch_alt): the restart origin -- attempt 1 starts its joints from it instead of a draw,
+        and every restart its base."""
         N = self._check_q(Q)
         _plan_device(sdf, Q)
-        if Q0 is not None:
-            _same_device(Q0, Q, "Q0")
-            if Q0.shape != Q.shape or Q0.stride() != Q.stride() or Q0.dtype != Q.dtype:
-                raise ValueError("Q0 must have Q's shape, strides and dtype")
+        for name, X in (("Q0", Q0), ("Q_alt", Q_alt)):
+            if X is not None:
+                _same_device(X, Q, name)
+                if X.shape != Q.shape or X.stride() != Q.stride() or X.dtype != Q.dtype:
+                    raise ValueError(f"{name} must have Q's shape, strides and dtype")
         if targets.shape != (12, N) or targets.dtype != self.dtype or not targets.is_contiguous():
             raise ValueError("targets must be a contiguous (12, N) tensor of the plan dtype")
         _same_device(targets, Q, "targets")
@@ -301,6 +304,7 @@ class CollisionIKPlan(Plan):
         cp = K.IkCollParams(float(margin), float(band), float(weight), float(feas))
         st = (stream or torch.cuda.current_stream(Q.device)).cuda_stream
         q0p = (Q0 if Q0 is not None else Q).data_ptr()
+        scene_p, lds = None, 0
         if isinstance(sdf, AttachedUnionSDF):
             if scene_q is None:
                 raise ValueError("an AttachedUnionSDF needs scene_q (its scene joint values)")
@@ -315,29 +319,38 @@ class CollisionIKPlan(Plan):
                 if scene_q.shape != (sdf.n_scene_cols, N) or scene_q.stride(1) != 1:
                     raise ValueError(f"scene_q must be ({sdf.n_scene_cols}, N) with unit target stride")
                 lds = scene_q.stride(0)
-            K.check(K.lib().kin_ik_coll_batch_scene(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
-                                                    scene_q.data_ptr() if scene_q.numel() else None, lds, q0p,
-                                                    Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N,
-                                                    st))
-            return Q, iters, err
-        if scene_q is not None:
+            scene_p = scene_q.data_ptr() if scene_q.numel() else None
+        elif scene_q is not None:
             raise ValueError("scene_q is only for an AttachedUnionSDF")
-        K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N, q0p,
-                                          Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N, st))
+        if Q_alt is not None:
+            K.check(K.lib().kin_ik_coll_batch_alt(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                                  scene_p, lds, q0p, Q_alt.data_ptr(), Q.data_ptr(), Q.stride(0), N,
+                                                  iters.data_ptr(), err.data_ptr(), N, st))
+        elif isinstance(sdf, AttachedUnionSDF):
+            K.check(K.lib().kin_ik_coll_batch_scene(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                                    scene_p, lds, q0p, Q.data_ptr(), Q.stride(0), N, iters.data_ptr(),
+                                                    err.data_ptr(), N, st))
+        else:
+            K.check(K.lib().kin_ik_coll_batch(self._h, sdf._h, C.byref(prm), C.byref(cp), targets.data_ptr(), N, q0p,
+                                              Q.data_ptr(), Q.stride(0), N, iters.data_ptr(), err.data_ptr(), N, st))
         return Q, iters, err
 
     def solve(self, sdf, targets: torch.Tensor, Q0: torch.Tensor, use_bistage=True, margin=0.02,
-              with_rot=2, max_iters=64, restarts=3, seed=0, index_base=0, stream=None, **kw):
+              with_rot=2, max_iters=64, restarts=3, seed=0, index_base=0, stream=None, alt_start=True, **kw):
         """Both stages on the device, no host round trip: stage 1 (use_bistage) = the collision-free
         DLS (kin_ik_dls_batch_from, the seeds read from Q0), stage 2 = kin_ik_coll_batch from its
-        result (src/inverse_kinematics.jl:1-21).  -> (Q, iters, err [3, N]) of stage 2."""
+        result (src/inverse_kinematics.jl:1-21).  -> (Q, iters, err [3, N]) of stage 2.
+        alt_start (with use_bistage and restarts >= 1): stage 2's restarts start from Q0, the pose stage 1
+        started from (kin_ik_coll_batch_alt: attempt 1 at Q0, later attempts drawn joints on Q0's base),
+        instead of from stage 1's answer, whose base stage 1 has moved."""
         Q = torch.empty_like(Q0)
         ik_kw = {k: v for k, v in kw.items() if k in ("lam", "tol_pos", "tol_rot", "max_step")}
         if use_bistage:
             self.ik_dls(targets, Q, Q0=Q0, max_iters=max_iters, restarts=restarts, seed=seed, with_rot=with_rot,
                         index_base=index_base, stream=stream, **ik_kw)
             return self.ik_coll(sdf, targets, Q, margin=margin, with_rot=with_rot, max_iters=max_iters,
-                                restarts=restarts, seed=seed, index_base=index_base, stream=stream, **kw)
+                                restarts=restarts, seed=seed, index_base=index_base, stream=stream,
+                                Q_alt=Q0 if alt_start else None, **kw)
         return self.ik_coll(sdf, targets, Q, Q0=Q0, margin=margin, with_rot=with_rot, max_iters=max_iters,
                             restarts=restarts, seed=seed, index_base=index_base, stream=stream, **kw)
 

@@ -270,7 +270,8 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
     ``solver="DLS"`` (default): stage 1 (use_bistage) is the collision-free solve with the reference's
     ftol_abs rule (``_dls_ik_ftol``), stage 2 the batched collision-aware kernel
     (``CollisionIKPlan.ik_coll``, kin_ik_coll_batch: the reference's rpy objective plus the
-    IneqConst(sscc, joints, sdf, 1, margin) sphere rows, 3 seeded restarts) on a batch of one, converged
+    IneqConst(sscc, joints, sdf, 1, margin) sphere rows, 3 restarts: with use_bistage the first from the
+    angles stage 1 started from (kin_ik_coll_batch_alt), the others seeded draws) on a batch of one, converged
     to |dp|, |d rpy| < 1e-6 with every sphere at >= margin - 1e-6 (status ``:FTOL_REACHED``).  When no
     attempt converges (a pose the constraint forbids) the kernel returns the attempt whose end state has
     the lowest merit |dp|^2 + |d rpy|^2 + max(0, margin - min d)^2 (the penalty problem's value; ties: the
@@ -281,6 +282,7 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
     from .collision import CollisionIKPlan
     from .mechanism import _dls_ik_ftol
 
+    q_start = np.asarray(m.get_joint_angles(joints), np.float64)  # stage 2's restart attempt 1 starts here
     if use_bistage:  # stage 1: the collision-free problem seeds stage 2 (src/inverse_kinematics.jl:8-13)
         _dls_ik_ftol(m, link, joints, target_pose, ftol, with_rot, max_iters, lam, max_step)
     n_dof = len(joints) + (3 if m.with_base else 0)
@@ -292,9 +294,10 @@ def collision_aware_ik(m: Mechanism, link: Link, joints, target_pose, sscc: Swep
         plan = CollisionIKPlan(sscc, link, joints, dtype=torch.float64)
         Q0 = torch.tensor(m.get_joint_angles(joints), dtype=torch.float64, device=dev).reshape(-1, 1).contiguous()
         Q = torch.empty_like(Q0)
+        Qa = torch.tensor(q_start, dtype=torch.float64, device=dev).reshape(-1, 1).contiguous() if use_bistage else None
         Q, it, err = plan.ik_coll(sdf, tg.contiguous(), Q, Q0=Q0, margin=margin, with_rot=2 if with_rot else 0,
                                   max_iters=max_iters, restarts=3, lam=lam, max_step=max_step, tol_pos=1e-6,
-                                  tol_rot=1e-6)
+                                  tol_rot=1e-6, Q_alt=Qa)
         q = Q[:, 0].cpu().numpy()
         m.set_joint_angles(joints, q)
         return q, (":FTOL_REACHED" if int(it[0]) <= max_iters else ":MAXEVAL_REACHED")

@@ -905,7 +905,8 @@ static void box_gradient_analytic(const or_union_sdf* s, int32_t k, const double
 void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, double* q, int64_t ldq, int32_t n_q,
                       const int32_t* qids, int32_t link_id, const double* target, int64_t ldt, const or_ik_params* prm,
                       const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii,
-                      const or_union_sdf* const* sdfs, int32_t* iters_out, double* err_out, int32_t n_threads) {
+                      const or_union_sdf* const* sdfs, const double* q_alt, int32_t* iters_out, double* err_out,
+                      int32_t n_threads) {
     int nt = nthreads_of(n_threads);
     const int32_t nd = n_q + (proto->with_base ? 3 : 0);
     const int rows = prm->with_rot ? 6 : 3;
@@ -1009,7 +1010,10 @@ void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, 
                     if (last) break;
                     const int32_t att = it / attempt_len;
                     for (int32_t c = 0; c < nd; ++c) {
-                        if (c < n_q && rel[c]) {
+                        if (q_alt && (c >= n_q || (att == 1 && rel[c]))) {
+                            /* kin_ik_coll_batch_alt: attempt 1 from the second start, every restart's base */
+                            a[c] = q_alt[c * ldq + i];
+                        } else if (c < n_q && rel[c]) {
                             double l = lo[c], h = hi[c];
                             if (!isfinite(l) || !isfinite(h)) { l = -3.14159265358979323846; h = 3.14159265358979323846; }
                             a[c] = l + (h - l) * or_ik_seed_u01(prm->seed, i, att, c);

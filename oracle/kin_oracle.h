@@ -150,11 +150,14 @@ void or_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, con
                    int64_t ldg, int32_t n_threads);
 
 /* build-defined collision-aware IK (kin_ik_coll_batch), restated: see kin_oracle.c.
- * cprm = {margin, band, weight, feas}; err_out [3][n]: |dp|, |rot|, min sphere distance. */
+ * cprm = {margin, band, weight, feas}; err_out [3][n]: |dp|, |rot|, min sphere distance.
+ * q_alt (nullable, [n_q(+3)][ldq]): restart attempt 1 starts the relevant joints from it instead of a draw,
+ * and every restart the base (kin_ik_coll_batch_alt). */
 void or_ik_coll_batch(const or_mech* proto, const or_union_sdf* sdf, int64_t n, double* q, int64_t ldq, int32_t n_q,
                       const int32_t* qids, int32_t link_id, const double* target, int64_t ldt, const or_ik_params* prm,
                       const double* cprm, int32_t n_sph, const int32_t* sph, const double* radii,
-                      const or_union_sdf* const* sdfs, int32_t* iters_out, double* err_out, int32_t n_threads);
+                      const or_union_sdf* const* sdfs, const double* q_alt, int32_t* iters_out, double* err_out,
+                      int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -197,7 +197,7 @@ def lib():
         L.or_union_sdf_value.argtypes = [P, P, P]
         L.or_union_sdf_gradient.argtypes = [P, P, P]
         L.or_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, P, D, P, I64, P, I64, I32]
-        L.or_ik_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, I64, P, P, I32, P, P, P, P, P, I32]
+        L.or_ik_coll_batch.argtypes = [P, P, I64, P, I64, I32, P, I32, P, I64, P, P, I32, P, P, P, P, P, P, I32]
         _lib = L
     return _lib
 
@@ -345,8 +345,10 @@ class OracleMech:
 
 def ik_coll_batch(mech: "OracleMech", sdf: "OracleUnionSDF", q0, q_joint_ids, link_id, target, sphere_links, radii,
                   margin=0.02, band=0.01, weight=1.0, feas=1e-6, max_iters=64, lam=1e-2, tol_pos=1e-3, tol_rot=1e-3,
-                  max_step=0.5, with_rot=2, restarts=0, seed=0, n_threads=0, sdfs=None, sphere_parents=None):
+                  max_step=0.5, with_rot=2, restarts=0, seed=0, n_threads=0, sdfs=None, sphere_parents=None,
+                  q_alt=None):
     """Restatement of kin_ik_coll_batch (stage 2 of the bistage collision-aware IK) -> (q, iters, err [3, N]).
+    `q_alt` (the layout of q0): kin_ik_coll_batch_alt's restart origin (attempt 1's joints, every restart's base).
     `sdfs`: one OracleUnionSDF per target (a scene mechanism's boxes at each target's scene state) instead of
     `sdf`.  `sphere_parents`: the tree links the sphere links hang off (add_new_link parents); with it the
     sphere rows are added in the kernel's order (ikc_sphere_order) -- the same sums in the same order."""
@@ -363,6 +365,8 @@ def ik_coll_batch(mech: "OracleMech", sdf: "OracleUnionSDF", q0, q_joint_ids, li
     err = np.zeros((3, N))
     prm = _IkParams(max_iters, lam, tol_pos, tol_rot, max_step, int(with_rot), int(restarts), int(seed))
     cp = _f64([margin, band, weight, feas])
+    qa = None if q_alt is None else _f64(q_alt)
+    assert qa is None or qa.shape == q.shape
     harr = None
     if sdfs is not None:
         assert len(sdfs) == N
@@ -370,7 +374,7 @@ def ik_coll_batch(mech: "OracleMech", sdf: "OracleUnionSDF", q0, q_joint_ids, li
     lib().or_ik_coll_batch(mech._h, (sdf or sdfs[0])._h, N, _p(q), N, ids.size, _p(ids), int(link_id), _p(tgt),
                            tgt.shape[1], C.byref(prm), _p(cp), sph.size, _p(sph) if sph.size else None,
                            _p(r) if sph.size else None, C.cast(harr, C.c_void_p) if harr is not None else None,
-                           _p(it), _p(err), n_threads)
+                           _p(qa) if qa is not None else None, _p(it), _p(err), n_threads)
     return q, it, err
 
 

@@ -92,7 +92,7 @@ class Scene:
         return [self.om.get_transform(s)[:3, 3] for s in self.sph]
 
     def check(self, link, tg, Q1, sdf, box=None, boxes=None, spec=False, lanes=0, scene_q=None, kw=KW,
-              min_conv=0.5, knife_edge=0.01):
+              min_conv=0.5, knife_edge=0.01, q_alt=None):
         """GPU vs oracle.  Equal iteration counts on all but `knife_edge` of the targets: a sphere the penalty
         holds at the band's edge (d -> margin + band, where its row switches on and off) sits on a
         switching surface, and last-bit differences between the kernel's FMA sums and the oracle's can
@@ -105,9 +105,11 @@ class Scene:
             plan.specialize()
         dev = Q1.device
         tgt = torch.tensor(tg, dtype=torch.float64, device=dev).contiguous()
-        Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, scene_q=scene_q, **kw)
+        Q, it, err = plan.ik_coll(sdf, tgt, torch.empty_like(Q1), Q0=Q1, lanes=lanes, scene_q=scene_q, Q_alt=q_alt,
+                                  **kw)
         rq, rit, rerr = self.O.ik_coll_batch(self.om, box, Q1.cpu().numpy(), self.ids, self.tree.link_id(link), tg,
-                                             self.sph, self.rad, sdfs=boxes, sphere_parents=self.par, **kw)
+                                             self.sph, self.rad, sdfs=boxes, sphere_parents=self.par,
+                                             q_alt=None if q_alt is None else q_alt.cpu().numpy(), **kw)
         it = it.cpu().numpy()
         q, e = Q.cpu().numpy(), err.cpu().numpy()
         conv = it <= kw["max_iters"]
@@ -217,10 +219,13 @@ def test_two_arm_tree(tmp_path, spec, lanes, with_base):
     assert (moved[conv & hit] > 1e-3).mean() > 0.5  # the right arm left the box
 
 
+@pytest.mark.parametrize("alt", [False, True])
 @pytest.mark.parametrize("spec", [False, True])
-def test_fetch_with_base_in_fridge(spec):
+def test_fetch_with_base_in_fridge(spec, alt):
     """Fetch with its planar base (8 joints + x, y, theta): stage 2 in the fridge scene of
-    test/test_inverse_kinematics.jl:52-86, the base a variable of every sphere row."""
+    test/test_inverse_kinematics.jl:52-86, the base a variable of every sphere row.  alt: a second start
+    pose per target (kin_ik_coll_batch_alt; random angles within the limits and base offsets) that restart
+    attempt 1 starts from, joints and base, on the GPU and in the oracle."""
     sc = Scene(golden("fetch.urdf"), ARM, kinhip.FETCH_ARM_SPHERES, with_base=True)
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(47)
@@ -228,7 +233,15 @@ def test_fetch_with_base_in_fridge(spec):
     tg = _fridge_targets(rng, N)
     Q1 = _stage1(sc, "gripper_link", tg, dev)
     sdf, box = _fridge_box()
-    sc.check("gripper_link", tg, Q1, sdf, box=box, spec=spec)
+    q_alt = None
+    if alt:
+        lo = np.array([j.lower_limit for j in sc.q])
+        hi = np.array([j.upper_limit for j in sc.q])
+        lo, hi = np.where(np.isfinite(lo), lo, -np.pi), np.where(np.isfinite(hi), hi, np.pi)
+        qa = np.concatenate([rng.uniform(lo[:, None], hi[:, None], (len(lo), N)),
+                             rng.uniform(-0.1, 0.1, (3, N))])
+        q_alt = torch.tensor(qa, dtype=torch.float64, device=dev).contiguous()
+    sc.check("gripper_link", tg, Q1, sdf, box=box, spec=spec, q_alt=q_alt)
 
 
 def test_door_angle_per_target():
@@ -388,6 +401,16 @@ def test_pr2_two_arms_with_base_door_per_target(spec, lanes):
     # the reference's acceptance on the converged targets: |dp| < 1e-3 and every sphere clear (vals > -1e-5)
     e = err.cpu().numpy()
     assert (e[0][conv] < 1e-3).all() and (e[2][conv] > KW["margin"] - 1e-5).all()
+    # the bistage form (CollisionIKPlan.solve): restart attempt 1 from the pose stage 1 started from
+    # (kin_ik_coll_batch_alt, q_alt = Q0) -- iterates vs the oracle again, and it converges at least as often
+    Qa, ita, erra = sc.check(link, tg, Q1, asdf, box=None, boxes=boxes, spec=spec, lanes=lanes, scene_q=scene_q,
+                             q_alt=Q0)
+    conva = ita <= KW["max_iters"]
+    print(f"PR2 door per target: converged {conv.mean():.3f}, with attempt 1 from the start pose {conva.mean():.3f}")
+    assert conva.mean() >= conv.mean()
+    a0 = torch.tensor(it <= KW["max_iters"] // (KW["restarts"] + 1), device=dev)  # solved by attempt 0: unchanged
+    assert torch.equal(Qa[:, a0], Q[:, a0]) and torch.equal(erra[:, a0], err[:, a0])
+    assert (ita[a0.cpu().numpy()] == it[a0.cpu().numpy()]).all()
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
@@ -416,6 +439,13 @@ def test_scene_specialized_equals_generic(dtype):
         got = spc.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q, lanes=lanes, **kw)
         for a, b in zip(got, ref):
             assert torch.equal(a, b), lanes
+    # with a second start pose (kin_ik_coll_batch_alt) for attempt 1: every layout still bit-identical
+    Qa = torch.zeros_like(Q1)
+    ref = gen.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q, lanes=1, Q_alt=Qa, **kw)
+    for lanes in (0, 1, 4, 16, 64):
+        got = spc.ik_coll(asdf, tgt, torch.empty_like(Q1), Q0=Q1, scene_q=scene_q, lanes=lanes, Q_alt=Qa, **kw)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b), ("alt", lanes)
 
 
 @pytest.mark.parametrize("with_base", [False, True])

@@ -264,7 +264,7 @@ def test_shim_collision_ik_with_attached_fridge():
     the reference's UnionSDF(fridge) (test/test_inverse_kinematics.jl:52-86, fridge_demo.jl:13-37): the shim's
     exact C-ABI sequence -- HIPSDF(fridge, [door_joint]) = kin_model_create + kin_sdf_create_attached;
     the cached plan = kin_coll_ik_plan_create + kin_plan_specialize(0); stage 1 kin_ik_dls_batch_from; stage 2
-    kin_ik_coll_batch_scene with one door angle per target (scene columns door, base x, y, theta) -- replayed
+    kin_ik_coll_batch_alt (restart attempt 1 from Q0) with one door angle per target (scene columns door, base x, y, theta) -- replayed
     through ctypes with the shim's default keywords, against the oracle: stage 1 or_ik_dls_batch, stage 2
     or_ik_coll_batch over each target's static fridge union (fp64, equal iteration counts, angles 1e-7)."""
     import oracle as O
@@ -322,9 +322,9 @@ def test_shim_collision_ik_with_attached_fridge():
     try:
         K.check(K.lib().kin_ik_dls_batch_from(p, C.byref(prm), targets.data_ptr(), N, Q0.data_ptr(), Q1.data_ptr(),
                                               N, N, iters.data_ptr(), err.data_ptr(), N, None))
-        K.check(K.lib().kin_ik_coll_batch_scene(p, sdf, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
-                                                scene_q.data_ptr(), N, Q1.data_ptr(), Q.data_ptr(), N, N,
-                                                iters.data_ptr(), err.data_ptr(), N, None))
+        K.check(K.lib().kin_ik_coll_batch_alt(p, sdf, C.byref(prm), C.byref(cp), targets.data_ptr(), N,
+                                              scene_q.data_ptr(), N, Q1.data_ptr(), Q0.data_ptr(), Q.data_ptr(), N,
+                                              N, iters.data_ptr(), err.data_ptr(), N, None))
         torch.cuda.synchronize()
     finally:
         K.lib().kin_plan_destroy(p)
@@ -344,7 +344,8 @@ def test_shim_collision_ik_with_attached_fridge():
     ft = O.parse_urdf_tree(golden("fridge.urdf"))
     boxes = [O.OracleUnionSDF(*O.fridge_boxes(ft, door_angle=dd, base=(1.2, 0.0, 0.0))) for dd in doors]
     rq, rit, rerr = O.ik_coll_batch(om, None, q1, oids, tree.link_id("gripper_link"), tg, osph, list(rad),
-                                    margin=0.02, band=0.0, weight=1.0, feas=1e-6, sdfs=boxes, sphere_parents=opar, **kw)
+                                    margin=0.02, band=0.0, weight=1.0, feas=1e-6, sdfs=boxes, sphere_parents=opar,
+                                    q_alt=np.zeros((8, N)), **kw)
     it = iters.cpu().numpy()
     same = it == rit
     assert (~same).mean() <= 0.01, (np.where(~same)[0], it[~same], rit[~same])
@@ -407,6 +408,7 @@ def ik_coll(hm, link_id, ids, T, sscc, sdf_h, use_bistage=True, ftol=1e-5, with_
     with_rot) for a static sdf (HIPSDF(UnionSDF) = kin_sdf_create_boxes), line for line.  `sscc` =
     (sphere link ids, radii)."""
     mech = hm.mech
+    q_start = angles_batch(mech, ids)
     if use_bistage:
         ik_ftol(hm, link_id, ids, T, ftol=ftol, with_rot=with_rot, max_iters=max_iters, lam=lam, max_step=max_step)
     sph, rad = sscc
@@ -418,8 +420,9 @@ def ik_coll(hm, link_id, ids, T, sscc, sdf_h, use_bistage=True, ftol=1e-5, with_
     err = torch.empty((3, 1), dtype=torch.float64, device=_dev())
     prm = K.IkParams(max_iters, lam, 1e-6, 1e-6, max_step, 2 if with_rot else 0, 3, 0, 0, 0, 0.0)
     cprm = K.IkCollParams(margin, 0.0, 1.0, 1e-6)
-    K.check(K.lib().kin_ik_coll_batch(p, sdf_h, C.byref(prm), C.byref(cprm), tgt.data_ptr(), 1, q0.data_ptr(),
-                                      q.data_ptr(), 1, 1, iters.data_ptr(), err.data_ptr(), 1, None))
+    K.check(K.lib().kin_ik_coll_batch_alt(p, sdf_h, C.byref(prm), C.byref(cprm), tgt.data_ptr(), 1, None, 0,
+                                          q0.data_ptr(), q_start.data_ptr() if use_bistage else None, q.data_ptr(),
+                                          1, 1, iters.data_ptr(), err.data_ptr(), 1, None))
     qv = q[:, 0].cpu().numpy()
     mech.set_joint_angles(ids, qv)
     return qv, (":FTOL_REACHED" if int(iters[0]) <= max_iters else ":MAXEVAL_REACHED")

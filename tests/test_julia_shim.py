@@ -125,7 +125,8 @@ def test_julia_struct_mirrors_c_struct(jl_name):
 
 RUN_ENTRIES = ("kin_plan_run", "kin_plan_run_tiled", "kin_ik_dls_batch", "kin_ik_dls_batch_from",
                "kin_point_ik_nakamura_batch", "kin_coll_batch", "kin_ineq_const_batch", "kin_pose_const_batch",
-               "kin_coll_batch_scene", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_ik_dls_batch_trace")
+               "kin_coll_batch_scene", "kin_ik_coll_batch", "kin_ik_coll_batch_scene", "kin_ik_dls_batch_trace",
+               "kin_ik_coll_batch_alt")
 
 
 def jl_functions(src):

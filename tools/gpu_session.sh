@@ -27,6 +27,7 @@
 #   coll-dump                   the specialised collision source (A/B build, KINHIP_JIT_DUMP) for offline ISA
 #   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
 #   pr2-miss[=<n>]              tools/pr2_miss_study.py (PR2 collision-IK leg misses vs host SLSQP)
+#   pr2-alt                     tools/pr2_alt_probe.py (stage-2 step budgets from the manip pose, alt schedules)
 #   scene-const                 door sweep A/B: scene tables as data vs compiled in (tools/scene_ab.py), x3 each,
 #                               plus a rocprofv3 kernel trace of both (VGPR counts)
 #   pts-probe                   tools/pts_probe (hipStreamPerThread after thread exit vs hipDeviceSynchronize)
@@ -63,6 +64,10 @@ for step in "$@"; do
       timeout -k 10 400 env KINHIP_LIB=$AB KINHIP_JIT_CODE_DUMP=$PWD/gpurun_out/isa/jit KINHIP_JIT_DUMP=$PWD/gpurun_out/isa/src \
         python bench.py --no-cpu > gpurun_out/isa/bench_ab.json 2> gpurun_out/isa/bench_ab.err || { tail gpurun_out/isa/bench_ab.err; exit 9; }
       python tools/isa_check.py gpurun_out/isa/jit.*.co > gpurun_out/isa/isa_check.txt 2>&1; tail -3 gpurun_out/isa/isa_check.txt ;;
+    pr2-alt)
+      timeout -k 10 600 python tools/pr2_alt_probe.py > gpurun_out/pr2_alt_probe.json 2> gpurun_out/pr2_alt_probe.err \
+        || { tail -20 gpurun_out/pr2_alt_probe.err; exit 12; }
+      cat gpurun_out/pr2_alt_probe.json ;;
     pr2-miss|pr2-miss=*)
       n=${step#pr2-miss}; n=${n#=}; n=${n:-200}
       timeout -k 10 900 python tools/pr2_miss_study.py $n > gpurun_out/pr2_miss_study.json 2> gpurun_out/pr2_miss_study.err \

@@ -74,9 +74,11 @@ for dt, name in ((torch.float32, "f32"), (torch.float64, "f64")):
     kw = dict(max_iters=128, restarts=3, seed=1, with_rot=2)
     Q1 = torch.empty_like(Q0)
     _, it1, err1 = cplan.ik_dls(T, Q1, Q0=Q0, **kw)
-    Q, it, err = cplan.solve(asdf, T, Q0, scene_q=SQ, **kw)
+    Q, it, err = cplan.solve(asdf, T, Q0, scene_q=SQ, **kw)  # (stage 2's attempt 1 from Q0: kin_ik_coll_batch_alt)
+    _, it_na, _ = cplan.solve(asdf, T, Q0, scene_q=SQ, alt_start=False, **kw)  # (round-6 start: every restart drawn)
     torch.cuda.synchronize()
     conv = (it <= 128).cpu().numpy()
+    out[f"converged_{name}_all_restarts_drawn"] = float((it_na <= 128).float().mean())
     res[name] = dict(Q1=Q1.double().cpu().numpy(), Q=Q.double().cpu().numpy(), conv=conv,
                      err=err.double().cpu().numpy(), stage1_conv=(it1 <= 128).cpu().numpy())
     out[f"converged_{name}"] = float(conv.mean())
