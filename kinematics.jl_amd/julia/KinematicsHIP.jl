@@ -680,6 +680,82 @@ function pose_const!(hm::HIPModel, link::Link, joints::Vector{<:Joint}, with_rot
     vals, jac
 end
 
-export HIPModel, sync!, batch_array, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!
+# --- the reference's plan_trajectory with the collision queries on the GPU (src/planning.jl:32-68, 332-401) ---
+
+const HIP_MODELS = WeakKeyDict{Mechanism,HIPModel}()
+
+"""The HIPModel of a Mechanism, made on first use and kept while the Mechanism lives: the reference's calls
+that reach the robot only through `sscc.mech` (IneqConst, compute_coll_dists) use it."""
+hip_model(m::Mechanism) = get!(() -> HIPModel(m), HIP_MODELS, m)
+
+"""`GPUSDF(sdf)`: a reference SDF (UnionSDF / BoxSDF, e.g. UnionSDF(fridge)) with its device snapshot
+HIPSDF(sdf).  It is an AbstractSDF, so the reference's own entry points take it unchanged --
+`plan_trajectory(sscc, joints, GPUSDF(sdf), q_start, q_goal, n_wp; margin, partial_consts, ftol_abs,
+solver)` -- and their collision queries run on the GPU:
+  * compute_coll_dists / compute_coll_dists_and_grads(sscc, joints, sdf; truncation_dist) and their `!`
+    forms (src/collision.jl:51-103) at the mechanism's current angles (kin_coll_batch, a batch of one);
+  * IneqConst (src/planning.jl:55-68) called with the dense Vector / Matrix buffers NLopt's and SciPy's
+    adapters pass (nloptize / scipynize, :225-247): all n_wp waypoints in one kin_ineq_const_batch launch.
+    Other buffers (Ipopt's views) take the reference's per-waypoint loop, whose queries are the GPU ones
+    above.  The mechanism is left at the last waypoint, as the reference's loop leaves it.
+Point queries (`sdf(p)`, gradient!) forward to the wrapped SDF; the snapshot is the scene at its angles
+when GPUSDF was made.  Distances use the analytic box gradient (the reference differentiates forward with
+eps 1e-7)."""
+struct GPUSDF <: Kinematics.AbstractSDF{Kinematics.IsStandAlone}
+    sdf::Kinematics.AbstractSDF
+    hip::HIPSDF
+end
+GPUSDF(sdf::Kinematics.AbstractSDF) = GPUSDF(sdf, HIPSDF(sdf))
+HIPSDF(s::GPUSDF) = s.hip
+(s::GPUSDF)(p; kw...) = s.sdf(p; kw...)
+Kinematics.gradient!(s::GPUSDF, p, out_grad::AbstractVector) = Kinematics.gradient!(s.sdf, p, out_grad)
+
+Kinematics.compute_coll_dists_and_grads(sscc::Kinematics.SweptSphereCollisionChecker, joints::Vector{<:Joint},
+                                        sdf::GPUSDF; truncation_dist=Inf) =
+    Kinematics.compute_coll_dists_and_grads(hip_model(sscc.mech), sscc, joints, sdf.hip;
+                                            truncation_dist=truncation_dist)
+
+Kinematics.compute_coll_dists(sscc::Kinematics.SweptSphereCollisionChecker, joints::Vector{<:Joint}, sdf::GPUSDF) =
+    Kinematics.compute_coll_dists(hip_model(sscc.mech), sscc, joints, sdf.hip)
+
+function Kinematics.compute_coll_dists_and_grads!(sscc::Kinematics.SweptSphereCollisionChecker,
+                                                  joints::Vector{<:Joint}, sdf::GPUSDF,
+                                                  out_vals::AbstractArray{Float64,1},
+                                                  out_grads::AbstractArray{Float64,2}; truncation_dist=Inf)
+    v, g = Kinematics.compute_coll_dists_and_grads(sscc, joints, sdf; truncation_dist=truncation_dist)
+    out_vals .= v
+    out_grads .= g
+    nothing
+end
+
+function Kinematics.compute_coll_dists!(sscc::Kinematics.SweptSphereCollisionChecker, joints::Vector{<:Joint},
+                                        sdf::GPUSDF, out_vals::AbstractArray{Float64,1})
+    out_vals .= Kinematics.compute_coll_dists(sscc, joints, sdf)
+    nothing
+end
+
+"""IneqConst over all waypoints at once when its sdf is a GPUSDF (see GPUSDF); any other IneqConst runs the
+reference's method unchanged (`invoke`)."""
+function (this::Kinematics.IneqConst)(xi::Vector{Float64}, val_vec::Vector{Float64}, jac_mat::Matrix{Float64})
+    this.sdf isa GPUSDF ||
+        return invoke(this, Tuple{AbstractVector,AbstractVector,AbstractMatrix}, xi, val_vec, jac_mat)
+    n_dof, n_wp, n_coll = this.n_dof, this.n_wp, this.n_coll
+    n_coll == 0 && return nothing
+    X = reshape(xi, n_dof, n_wp)
+    Xi = ROCMatrix{Float64}(permutedims(X))  # (n_wp, n_dof): waypoint index fastest, the C-ABI's batch
+    vals = ROCMatrix{Float64}(undef, n_wp, n_coll)
+    jac = ROCArray{Float64}(undef, n_wp, n_dof, n_coll)
+    ineq_const!(hip_model(this.sscc.mech), this.sscc, this.joints, this.sdf.hip, this.margin, Xi, vals, jac)
+    v = Array(vals)
+    J = Array(jac)
+    for i in 1:n_wp  # the reference's block-diagonal layout (:63-66)
+        val_vec[1+n_coll*(i-1):n_coll*i] = v[i, :]
+        jac_mat[1+n_dof*(i-1):n_dof*i, 1+n_coll*(i-1):n_coll*i] = J[i, :, :]
+    end
+    set_joint_angles(this.sscc.mech, this.joints, X[:, n_wp])
+    nothing
+end
+
+export HIPModel, sync!, batch_array, get_jacobian_tiled!, point_inverse_kinematics_nakamura!, HIPSDF, compute_coll_dists_and_grads!, ineq_const!, pose_const!, GPUSDF, hip_model
 
 end # module

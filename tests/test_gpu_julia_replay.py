@@ -613,3 +613,132 @@ def test_python_mirror_reference_pr2_with_collision(spheres):
     assert np.linalg.norm(_pose2angles(pose_target) - _pose2angles(pose_actual)) < 1e-3
     vals = kinhip.compute_coll_dists(sscc, joints, sdf)
     assert np.all(vals > -1e-5), vals
+
+
+# ---- the reference's plan_trajectory through GPUSDF (KinematicsHIP.jl "plan_trajectory with the collision
+# queries on the GPU") ----
+
+def gpusdf_ineq_const(hm, sscc, ids, sdf_h, margin, n_dof, n_wp, xi, val_vec, jac_mat):
+    """KinematicsHIP.jl (this::IneqConst)(xi::Vector, val_vec::Vector, jac_mat::Matrix) for a GPUSDF, line for
+    line: X = reshape(xi, n_dof, n_wp); Xi = permutedims(X) on the device ((n_wp, n_dof) column-major: row d of a
+    C-contiguous (n_dof, n_wp) array); coll_plan! + kin_ineq_const_batch; the block-diagonal fill; the
+    mechanism left at the last waypoint."""
+    sph, rad = sscc
+    n_coll = len(sph)
+    if n_coll == 0:
+        return
+    X = np.asarray(xi, np.float64).reshape(n_wp, n_dof).T  # Julia reshape(xi, (n_dof, n_wp))
+    Xi = torch.tensor(np.ascontiguousarray(X), dtype=torch.float64, device=_dev())
+    vals = torch.empty((n_coll, n_wp), dtype=torch.float64, device=_dev())         # Julia (n_wp, n_coll)
+    jac = torch.empty((n_coll, n_dof, n_wp), dtype=torch.float64, device=_dev())   # Julia (n_wp, n_dof, n_coll)
+    p = hm.coll_plan(sph, rad, ids)
+    K.check(K.lib().kin_ineq_const_batch(p, sdf_h, float(margin), Xi.data_ptr(), n_wp, n_wp, vals.data_ptr(), n_wp,
+                                         jac.data_ptr(), n_wp, None))
+    v, J = vals.cpu().numpy(), jac.cpu().numpy()
+    for i in range(n_wp):
+        val_vec[n_coll * i:n_coll * (i + 1)] = v[:, i]
+        jac_mat[n_dof * i:n_dof * (i + 1), n_coll * i:n_coll * (i + 1)] = J[:, :, i].T  # Julia J[i, :, :]
+    hm.mech.set_joint_angles(ids, X[:, -1])
+
+
+PLANNING_COLL_LINKS = ["wrist_flex_link", "torso_lift_link", "upperarm_roll_link", "elbow_flex_link"]
+
+
+@pytest.mark.parametrize("with_base", [False, True])
+def test_replay_reference_planning_through_gpusdf(with_base):
+    """test/test_planning.jl's planning_test(with_base, :SCIPY) with `boxsdf` wrapped as GPUSDF(boxsdf): the
+    reference's plan_trajectory (src/planning.jl:332-401) unchanged -- its compute_coll_dists asserts on the
+    start and goal (the GPUSDF method: the shim's compute_coll_dists(hm, ...)), construct_problem, the :SCIPY
+    minimize(f, xi_init, SLSQP, [ineq g, eq h], ftol) with g = scipynize(IneqConst), whose call is the shim's
+    batched GPUSDF method (replayed above).  Asserted: the replayed IneqConst equals the Python mirror's bit
+    for bit and the oracle's restatement (values 1e-9), at the straight line and at the answer; SLSQP succeeds;
+    the answer keeps its end points and every waypoint satisfies the reference's :NLOPT check
+    (compute_coll_dists .> -1e-2).  The spheres are build-defined (FETCH_LINK_SPHERES) and so the goal is the
+    first collision-free batched IK answer for the reference's target (as tests/test_planning.py)."""
+    from scipy.optimize import minimize
+
+    path = golden("fetch.urdf")
+    mech = Mech(path, with_base=with_base)
+    sph, rad, osph = [], [], []
+    tree = O.parse_urdf_tree(path)
+    om = O.OracleMech(tree, with_base=with_base)
+    for n in PLANNING_COLL_LINKS:  # add_coll_links(sscc, find_link(mech, n)) (src/collision.jl:39-49)
+        for c, r in kinhip.FETCH_LINK_SPHERES[n]:
+            name = f"{n}_sphere_{len(sph)}"
+            mech.add_new_link(name, mech.m.find_link(n), _transform(c))
+            sph.append(mech.m.find_link(name).id)
+            rad.append(r)
+            osph.append(om.add_new_link(tree.link_id(n), _transform(c)))
+    sscc = (sph, rad)
+    joints = [mech.m.find_joint(n).id for n in ARM]
+    n_dof = len(joints) + (3 if with_base else 0)
+    boxsdf = kinhip.UnionSDF([kinhip.BoxSDF(_transform((0.4, -0.25, 0.7)), (0.05, 0.05, 0.5))])  # HIPSDF(boxsdf)
+    obox = O.OracleUnionSDF([_transform((0.4, -0.25, 0.7))], [[0.05, 0.05, 0.5]])
+    # the mirror's IneqConst on its own mechanism with the same spheres
+    mm = kinhip.parse_urdf(path, with_base=with_base)
+    msscc = kinhip.SweptSphereCollisionChecker(mm)
+    for n in PLANNING_COLL_LINKS:
+        kinhip.add_coll_links(msscc, mm.find_link(n))
+    mjoints = [mm.find_joint(n) for n in ARM]
+    n_wp, margin = 10, 2e-2
+    hm = HIPModel(mech)
+    try:
+        q_start = mech.get_joint_angles(joints)
+        # goal: the first collision-free answer of a batched IK for (0.3, -0.4, 1.2) without rotation
+        gl = mm.find_link("gripper_link")
+        plan = mm.plan(mjoints, out_links=[gl], jac_link=gl, jac_joints=mjoints, dtype=torch.float64)
+        N = 256
+        g = torch.Generator().manual_seed(11)
+        Q0 = (torch.rand((n_dof, N), generator=g, dtype=torch.float64) * 2 - 1).to(_dev())
+        if with_base:
+            Q0[8:] = 0.0
+        tgt = torch.tensor(np.repeat(_transform((0.3, -0.4, 1.2))[:3, :4].T.reshape(12, 1), N, axis=1), device=_dev())
+        Q, it, _ = plan.ik_dls(tgt, Q0.contiguous(), with_rot=False, max_iters=64)
+        _, _, mn = msscc.plan(mjoints, dtype=torch.float64).run(boxsdf, Q, dists=False, min_dist=True)
+        ok = ((it <= 64) & (mn > 0.05)).nonzero()
+        assert ok.numel() > 0
+        q_goal = Q[:, int(ok[0, 0])].cpu().numpy()
+        # plan_trajectory(sscc, joints, GPUSDF(boxsdf), q_start, q_goal, n_wp; ftol_abs=1e-5, solver=:SCIPY)
+        for q in (q_start, q_goal):
+            mech.set_joint_angles(joints, q)
+            assert np.all(compute_coll_dists(hm, sscc, joints, boxsdf._h) > 0.0)
+        xi_init = kinhip.create_straight_trajectory(q_start, q_goal, n_wp)
+        F = kinhip.Objective(n_wp, np.ones(n_dof))
+        H = kinhip.EqConst(n_wp, [kinhip.ConfigurationConstraint(1, n_dof, q_start),
+                                  kinhip.ConfigurationConstraint(n_wp, n_dof, q_goal)])
+        g_val = np.zeros(n_wp * len(sph))
+        g_jac = np.zeros((n_dof * n_wp, n_wp * len(sph)))
+        G = kinhip.IneqConst(msscc, mjoints, boxsdf, n_wp, margin)
+
+        def check_g(xi):
+            gpusdf_ineq_const(hm, sscc, joints, boxsdf._h, margin, n_dof, n_wp, xi, g_val, g_jac)
+            G(xi, G.val_vec, G.jac_mat)
+            assert np.array_equal(g_val, G.val_vec) and np.array_equal(g_jac, G.jac_mat)
+            rv, _ = O.ineq_const(om, obox, xi, [tree.joint_id(n) for n in ARM], osph, rad, n_wp, margin)
+            np.testing.assert_allclose(g_val, rv, atol=1e-9)
+            np.testing.assert_array_equal(mech.get_joint_angles(joints), np.asarray(xi).reshape(n_wp, n_dof)[-1])
+
+        check_g(xi_init)
+        grad = np.zeros(xi_init.size)
+
+        def g_fun(xi):
+            gpusdf_ineq_const(hm, sscc, joints, boxsdf._h, margin, n_dof, n_wp, xi, g_val, g_jac)
+            return g_val.copy()
+
+        def h_fun(xi):
+            H(xi, H.val_vec, H.jac_mat)
+            return H.val_vec.copy()
+
+        cons = [{"type": "ineq", "fun": g_fun, "jac": lambda xi: (g_fun(xi), g_jac.T.copy())[1]},
+                {"type": "eq", "fun": h_fun, "jac": lambda xi: (h_fun(xi), H.jac_mat.T.copy())[1]}]
+        res = minimize(lambda x: F(x, grad), xi_init, method="SLSQP", constraints=cons, options={"ftol": 1e-5})
+        assert res.success, res.message
+        q_seq = res.x.reshape(n_wp, n_dof).T
+        np.testing.assert_allclose(q_seq[:, 0], q_start, atol=1e-6)
+        np.testing.assert_allclose(q_seq[:, -1], q_goal, atol=1e-6)
+        check_g(res.x)
+        for i in range(n_wp):  # the reference's :NLOPT checks (test_planning.jl:39-44)
+            mech.set_joint_angles(joints, q_seq[:, i])
+            assert np.all(compute_coll_dists(hm, sscc, joints, boxsdf._h) > -1e-2), i
+    finally:
+        hm.close()

@@ -181,6 +181,12 @@ KINEMATICS_EXPORTS = {
     "add_frame", "to_affine_map", "create_vis_sphere", "add_sdf", "MechanismVisualizer", "create_straight_trajectory",
     "plan_trajectory", "PoseConstraint", "ConfigurationConstraint", "inverse_kinematics!", "load_pr2", "rarm_joints",
     "larm_joints", "rarm_collision_links", "larm_collision_links", "reset_manip_pose", "__skrobot__"}
+# Kinematics.jl names the shim reaches qualified that the package does not export (defined, not exported):
+KINEMATICS_INTERNAL = {
+    "AbstractSDF": "src/sdf.jl:8", "IsStandAlone": "src/sdf.jl:2", "inv_pose": "src/sdf.jl:22-32",
+    "gradient!": "src/sdf.jl:34-41, 116-119", "IneqConst": "src/planning.jl:32-68", "Joint": "src/mechanism.jl:74",
+    "BoxMetaData": "src/mechanism.jl:3", "Fixed": "src/mechanism.jl:70", "Revolute": "src/mechanism.jl:52",
+    "Prismatic": "src/mechanism.jl:52", "lower_limit": "src/mechanism.jl:71-88", "upper_limit": "src/mechanism.jl:71-88"}
 JULIA_BUILTIN_TYPES = {"Vector", "Ptr", "Int32", "Int64", "Int", "UInt32", "UInt64", "Float32", "Float64", "Bool", "Union",
                        "Type", "Integer", "Real", "Dict", "Cint", "Cvoid", "Cstring", "Ref", "Nothing", "Any", "Tuple",
                        "Array", "Matrix", "SubArray", "AbstractMatrix", "AbstractArray", "AbstractVector", "Symbol"}
@@ -203,4 +209,14 @@ def test_type_names_in_signatures_resolve():
     bad = sorted(n for n in used
                  if not n.startswith(("Kinematics.", "AMDGPU."))
                  and n not in JULIA_BUILTIN_TYPES | amdgpu | defined | imported | KINEMATICS_EXPORTS)
+    assert not bad, bad
+
+
+def test_qualified_kinematics_names_exist():
+    """Every `Kinematics.X` the shim names (methods it extends, types it dispatches on) is one of Kinematics.jl's
+    exports or a name the package defines without exporting (KINEMATICS_INTERNAL, with its file)."""
+    code = "\n".join(line.split("#", 1)[0] for line in open(SHIM).read().splitlines())
+    code = re.sub(r'"""(.*?)"""', "", code, flags=re.S)  # (docstrings name Kinematics.jl, the package)
+    used = set(re.findall(r"Kinematics\.([A-Za-z_][\w!]*)", code))
+    bad = sorted(n for n in used if n not in KINEMATICS_EXPORTS and n not in KINEMATICS_INTERNAL)
     assert not bad, bad
