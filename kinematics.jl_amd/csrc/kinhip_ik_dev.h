@@ -703,7 +703,8 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             // reciprocal square root of each pivot and multiplies: the 6 square roots and 27 divisions
             // of the IEEE form are ~10 instructions each and dominated the iteration -- v_rsq_f32 for an
             // fp32 solve, v_rsq_f64 plus one Newton step (~2^-44) for its fp64 solve.  The fp64 kernel
-            // keeps the oracle's exact form (its iterates are compared with or_ik_dls_batch to 1e-7).
+            // takes the IEEE square root and one IEEE reciprocal per pivot, which multiplies (6 divisions
+            // instead of 27; the oracle's chol_solve, iterates compared with or_ik_dls_batch to 1e-7).
             constexpr bool fast = sizeof(T) == 4;
             auto rsq = [](TS d) -> TS {
                 if constexpr (sizeof(TS) == 4) {
@@ -724,14 +725,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                 } else {
                     d = sqrt_t(d);
                     A[j][j] = d;
+                    ip[j] = TS(1) / d;
                 }
 #pragma unroll
                 for (int r = j + 1; r < ROWS; ++r) {
                     TS sm = A[r][j];
 #pragma unroll
                     for (int k = 0; k < j; ++k) sm = fma(-A[r][k], A[j][k], sm);
-                    if constexpr (fast) A[r][j] = sm * ip[j];
-                    else A[r][j] = sm / d;
+                    A[r][j] = sm * ip[j];
                 }
             }
             auto chol_solve = [&](const TS (&rhs)[ROWS], TS (&x)[ROWS]) {
@@ -740,16 +741,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
                     TS sm = rhs[r];
 #pragma unroll
                     for (int k = 0; k < r; ++k) sm = fma(-A[r][k], x[k], sm);
-                    if constexpr (fast) x[r] = sm * ip[r];
-                    else x[r] = sm / A[r][r];
+                    x[r] = sm * ip[r];
                 }
 #pragma unroll
                 for (int r = ROWS - 1; r >= 0; --r) {
                     TS sm = x[r];
 #pragma unroll
                     for (int k = r + 1; k < ROWS; ++k) sm = fma(-A[k][r], x[k], sm);
-                    if constexpr (fast) x[r] = sm * ip[r];
-                    else x[r] = sm / A[r][r];
+                    x[r] = sm * ip[r];
                 }
             };
             TS e_s[ROWS], y0[ROWS];

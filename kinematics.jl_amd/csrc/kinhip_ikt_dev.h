@@ -745,7 +745,8 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         else restrict_to(active & ~held);  // (the generic kernels: one copy of the run-time masking)
         // Cholesky (in place, lower) and the two triangular solves.  fp32: the reciprocal square root of
         // each pivot (v_rsq_f32) multiplies instead of the IEEE square root and divisions (~10 instructions
-        // each, on the one-wave critical path); fp64 keeps the oracle's exact form (iterates to 1e-7)
+        // each, on the one-wave critical path); fp64: the IEEE square root and one IEEE reciprocal per pivot,
+        // which multiplies (the oracle's chol_solve; iterates to 1e-7)
         constexpr bool fast = sizeof(T) == 4;
         T ip[MAXV];
 #pragma unroll
@@ -761,6 +762,7 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 d = sqrt_t(d);
                 A[j][j] = d;
                 id = T(1) / d;
+                ip[j] = id;
             }
 #pragma unroll
             for (int r = j + 1; r < MAXV; ++r) {
@@ -775,16 +777,14 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             T sm = y[r];
 #pragma unroll
             for (int k = 0; k < r; ++k) sm = fnz(A[r][k], y[k], sm);
-            if constexpr (fast) y[r] = sm * ip[r];
-            else y[r] = sm / A[r][r];
+            y[r] = sm * ip[r];
         }
 #pragma unroll
         for (int r = MAXV - 1; r >= 0; --r) {
             T sm = y[r];
 #pragma unroll
             for (int k = r + 1; k < MAXV; ++k) sm = fnz(A[k][r], y[k], sm);
-            if constexpr (fast) y[r] = sm * ip[r];
-            else y[r] = sm / A[r][r];
+            y[r] = sm * ip[r];
         }
         KIN_IKT_STAMP(6);
         T mx = T(0);

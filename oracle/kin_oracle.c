@@ -629,28 +629,31 @@ void or_rot_error(const double* tgt16, const double* now16, double* w3) {
     rot_error(&a, &b, w3);
 }
 
-/* Cholesky solve of symmetric positive definite A (n x n, col-major), in place on b */
+/* Cholesky solve of symmetric positive definite A (n x n, col-major, n <= 64), in place on b.  Each pivot's
+ * reciprocal 1 / sqrt(d) is formed once and multiplies (the kernels' fp64 form: k_ik_dls, k_ik_tree). */
 static void chol_solve(double* A, int n, double* b) {
+    double ip[64];
     for (int j = 0; j < n; ++j) {
         double d = A[j + n * j];
         for (int k = 0; k < j; ++k) d -= A[j + n * k] * A[j + n * k];
         d = sqrt(d);
         A[j + n * j] = d;
+        ip[j] = 1.0 / d;
         for (int i = j + 1; i < n; ++i) {
             double s = A[i + n * j];
             for (int k = 0; k < j; ++k) s -= A[i + n * k] * A[j + n * k];
-            A[i + n * j] = s / d;
+            A[i + n * j] = s * ip[j];
         }
     }
     for (int i = 0; i < n; ++i) {
         double s = b[i];
         for (int k = 0; k < i; ++k) s -= A[i + n * k] * b[k];
-        b[i] = s / A[i + n * i];
+        b[i] = s * ip[i];
     }
     for (int i = n - 1; i >= 0; --i) {
         double s = b[i];
         for (int k = i + 1; k < n; ++k) s -= A[k + n * i] * b[k];
-        b[i] = s / A[i + n * i];
+        b[i] = s * ip[i];
     }
 }
 

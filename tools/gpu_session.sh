@@ -24,6 +24,7 @@
 #   ik-dump                     the specialised IK source (A/B build, KINHIP_JIT_DUMP) + a kernel trace of config 4
 #   coll                        the plain-row padding A/B of the config-5 legs (tools/coll_pad_ab.py)
 #   cik                         the f3 bistage IK leg split by stage, stage 2 on one lane vs 4 (tools/cik_bench.py)
+#   dumps                       the specialised IK (fp32 + fp64) and collision-IK sources (A/B build, KINHIP_JIT_DUMP)
 #   coll-dump                   the specialised collision source (A/B build, KINHIP_JIT_DUMP) for offline ISA
 #   ab=<workload>:<setting>[;<setting>...]   tools/ab.py (A/B build), e.g. ab=ik:base;KINHIP_IK_P2_WAVES=4
 #   pr2-miss[=<n>]              tools/pr2_miss_study.py (PR2 collision-IK leg misses vs host SLSQP)
@@ -147,6 +148,12 @@ for step in "$@"; do
         python -u tools/ik_ab.py 2>&1 | quiet || exit 8
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ikprof -o ik -- python3 -u tools/ik_ab.py \
         > gpurun_out/ikprof/run.log 2>&1 || exit 7 ;;
+    dumps)  # the specialised IK sources (both precisions) and the collision-IK ones, for offline ISA work
+      mkdir -p gpurun_out/jit
+      timeout -k 10 200 env KINHIP_LIB=$AB KINHIP_JIT_DUMP=$PWD/gpurun_out/jit/ik AB_SPEC=1 IK_N=65536 \
+        python -u tools/ik_ab.py 2>&1 | quiet || exit 8
+      timeout -k 10 300 env KINHIP_LIB=$AB KINHIP_JIT_DUMP=$PWD/gpurun_out/jit/cik AB_SPEC=1 \
+        python -u tools/cik_ab.py 2>&1 | quiet || exit 8 ;;
     coll)
       timeout -k 10 200 python -u tools/coll_pad_ab.py 2>&1 | quiet || exit 8 ;;
     cik)
