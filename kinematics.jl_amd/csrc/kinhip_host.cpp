@@ -2035,6 +2035,29 @@ int kin_pose_const_batch(const kin_plan* p, const void* target, int64_t ldt, con
     return KIN_OK;
 }
 
+// The state of scratch set k's last call: hipSuccess once it has completed, hipErrorNotReady while it runs, with
+// `wait` a host wait for it first.  An event last recorded on hipStreamPerThread by a thread that has since exited
+// can report an error instead (hipErrorCapturedEvent: this runtime consults the recording stream, destroyed with
+// its thread -- seen once in a full GPU suite, profiles/r06_gpu_tests_capturedevent.log).  That thread's exit
+// drained its per-thread stream (tools/pts_probe.hip), so the call has completed: the error is cleared, the set
+// gets a fresh event, and the result is hipSuccess.  Any other error is returned.  (Caller: the set is its own --
+// ik_mu held, or ik_busy.)
+static hipError_t ik_set_state(const kin_plan* p, int k, bool wait) {
+    hipError_t e = hipEventQuery(p->ik_ev[k]);
+    if (e == hipErrorNotReady && wait) e = hipEventSynchronize(p->ik_ev[k]);
+    if (e != hipSuccess && e != hipErrorNotReady && p->ik_stream[k] == (void*)hipStreamPerThread) {
+        (void)hipGetLastError();
+        hipEvent_t fresh = nullptr;
+        if (hipEventCreateWithFlags(&fresh, hipEventDisableTiming) == hipSuccess) {
+            (void)hipEventDestroy(p->ik_ev[k]);
+            (void)hipGetLastError();
+            p->ik_ev[k] = fresh;
+        }
+        e = hipSuccess;
+    }
+    return e;
+}
+
 static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void* target, int64_t ldt, const void* q0,
                         void* q, int64_t ldq, int64_t n, int32_t* iters, void* err, int64_t lde, void* stream,
                         void* trace = nullptr, int64_t ldtr = 0) {
@@ -2083,7 +2106,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
         if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
         const bool capturing = cs == hipStreamCaptureStatusActive;
         int set = -1;
-        hipEvent_t wait_ev = nullptr;  // the set's previous call ran on another stream: its event
+        int wait_set = -1;  // the set's previous call ran on another stream: order this call after it
         {
             std::unique_lock<std::mutex> lk(p->ik_mu);
             if (!p->d_ikscr) {
@@ -2112,7 +2135,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
                         if (!p->ik_busy[k] && !per_thread && p->ik_ev[k] && p->ik_stream[k] == stream) set = k;
                     for (int k = 0; k < kin_plan::kIkEagerSets && set < 0; ++k)
-                        if (!p->ik_busy[k] && (!p->ik_ev[k] || hipEventQuery(p->ik_ev[k]) == hipSuccess)) set = k;
+                        if (!p->ik_busy[k] && (!p->ik_ev[k] || ik_set_state(p, k, false) == hipSuccess)) set = k;
                     for (int k = 0; k < kin_plan::kIkEagerSets; ++k)
                         if (!p->ik_busy[k] && (lru < 0 || p->ik_tick[k] < p->ik_tick[lru])) lru = k;
                     if (set < 0) set = lru;
@@ -2128,7 +2151,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
                     ee = hipEventCreateWithFlags(&p->ik_ev[set], hipEventDisableTiming);
                     if (ee != hipSuccess) p->ik_ev[set] = nullptr;
                 } else if (per_thread || p->ik_stream[set] != stream) {
-                    wait_ev = p->ik_ev[set];  // (after the lock: see below)
+                    wait_set = set;  // (after the lock: see below)
                 }
                 if (ee != hipSuccess)
                     return set_error(KIN_E_DEVICE, std::string("kin_ik_dls_batch: two-phase scratch set: ") +
@@ -2144,7 +2167,7 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
             }
         }
         if (set >= 0 && !capturing) eager_set = set;
-        if (wait_ev) {
+        if (wait_set >= 0) {
             // Order this call after the set's previous call on another stream (or another thread's per-thread
             // stream): nothing to do once that call has finished, else a host wait for it, outside the lock (the
             // set is ours: ik_busy).  Not hipStreamWaitEvent: on this runtime, waiting on an event last recorded
@@ -2152,9 +2175,9 @@ static int ik_dls_batch(const kin_plan* p, const kin_ik_params* prm, const void*
             // state (its later events report hipErrorCapturedEvent, legacy-stream work fails "not permitted when
             // capturing": tools/pts_probe.hip, profiles/r06_pts_probe.txt); the event itself stays valid for
             // hipEventQuery / hipEventSynchronize, and a thread's exit drains its per-thread stream (same probe).
-            hipError_t ee = hipEventQuery(wait_ev);
+            hipError_t ee = ik_set_state(p, wait_set, false);
             if (ee == hipErrorNotReady) {
-                ee = hipEventSynchronize(wait_ev);
+                ee = ik_set_state(p, wait_set, true);
                 std::lock_guard<std::mutex> lk(p->ik_mu);
                 ++p->ik_stats.set_waits;
             }

@@ -661,15 +661,23 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int s = 0; s < MAXA; ++s) {
                 T J[ROWS];
                 jcol_pre<T, ROWS>(S[s], ro[s], rz[s], J);
-                if ((S[s].flags & SF_REC) && S[s].qcol >= 0) {  // (a constant in specialised kernels)
-                    const T ws = (blk >> s) & 1u ? T(0) : T(1);
+                const bool wt = (S[s].flags & SF_REC) && S[s].qcol >= 0;  // (a constant in specialised kernels)
+                const T ws = wt && ((blk >> s) & 1u) ? T(0) : T(1);
+                if (wt && !pk) {
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r) J[r] *= ws;
                 }
                 const int nr = (ROWS == 6 && S[s].jkind == MOT_PRISM) ? 3 : ROWS;  // prismatic: linear block only
                 if constexpr (pk) {
-                    const f2 Jp[3] = {f2{(float)J[0], (float)J[1]}, f2{(float)J[2], (float)J[3]},
-                                      f2{(float)J[4], (float)J[5]}};
+                    // the weight on the pair operand only (3 packed multiplies instead of 6): fma(J_r, ws J_c, a)
+                    // equals fma(ws J_r, ws J_c, a) for ws in {0, 1} (a held column adds an exact zero; the sums
+                    // are never -0), so every kernel variant keeps identical results
+                    f2 Jp[3] = {f2{(float)J[0], (float)J[1]}, f2{(float)J[2], (float)J[3]},
+                                f2{(float)J[4], (float)J[5]}};
+                    if (wt) {
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) Jp[k] = Jp[k] * f2{(float)ws, (float)ws};
+                    }
 #pragma unroll
                     for (int r = 0; r < ROWS; ++r)
 #pragma unroll

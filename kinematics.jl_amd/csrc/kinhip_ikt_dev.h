@@ -341,6 +341,37 @@ __device__ __forceinline__ void ikt_start(const KIkcProg<T>& P, const IkArgsT<T>
 #ifndef KINHIP_IKT_OWN
 #define KINHIP_IKT_OWN 0
 #endif
+// S > 1 (default): the normal equations distributed over the group's lanes through LDS.  Each sphere lane
+// stores its rows (w^2 a, a, viol), every lane the pose rows J (and e); lane sl then forms the entries sl,
+// sl + S, ... of the system -- entry (r, c) = sum over the in-band spheres, in sphere order, of
+// fma(w^2 a_k[r], a_k[c], .), then over the pose rows, in row order, of fma(J[i][r], J[i][c], .); the
+// right-hand side is column MAXV (a_k[MAXV] = viol_k, J[i][MAXV] = e_i) -- the same FMAs in the same order as
+// the one-lane kernel, so the results stay identical for every S -- and the group reads the assembled system
+// back for the (replicated) factorisation.  The replicated form broadcast every in-band sphere row by DPP and
+// had every lane form every entry: ~50 instructions per in-band sphere and ~300 for the pose rows on the
+// one-wave critical path of the batch's slowest target (offline ISA of the f3 kernel).  The masks of the
+// one-lane form (a sphere's variables, the target's) are left out: a row is 0 outside them, and fma(0, x, s)
+// = s for the finite, never negative-zero sums here.  0: the replicated form (A/B build).
+#ifndef KINHIP_IKT_LDSNE
+#define KINHIP_IKT_LDSNE 1
+#endif
+// LDS layout of one attempt group's system (elements of T): NSR sphere rows [w^2 a (MAXV), a (MAXV), viol]
+// padded to RW, ROWS pose rows [J (MAXV), e] padded to JW, then the NE assembled entries (row r: c = 0..r, rhs)
+template <int MAXV, int ROWS, int NSR>
+struct IktNe {
+    static constexpr int RW = (2 * MAXV + 1 + 3) & ~3;
+    static constexpr int JW = (MAXV + 1 + 3) & ~3;
+    static constexpr int NE = MAXV * (MAXV + 3) / 2;
+    static constexpr int JB = NSR * RW;
+    static constexpr int NB = JB + ROWS * JW;
+    static constexpr int SIZE = (NB + NE + 3) & ~3;
+    static constexpr int st(int r) { return r * (r + 3) / 2; }  // first entry of row r
+};
+template <typename T, int N>
+__device__ __forceinline__ T* ikt_ne_lds() {
+    __shared__ __attribute__((aligned(16))) T buf[N];
+    return buf;
+}
 template <typename T, int MAXV, int ROWS, int G, int S, int NR, int MAXG>
 __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>* __restrict__ St,
                                          const KSphere<T>* __restrict__ sph, const KBox<T>* __restrict__ boxes,
@@ -411,6 +442,32 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
     uint64_t sect_acc = 0, sect_prev = 0, sect_t0 = 0;
 #endif
     const uint32_t active = P.free_mask;
+    // KINHIP_IKT_LDSNE: this group's LDS region and this lane's entries of the system (row eR, column eC;
+    // eC = MAXV: the right-hand side; entries past NE are read but never stored)
+    // (trees of at most 12 variables: a two-arm tree's dense system of 170 entries measured 0.68 -> 0.91 ms
+    // on PR2, whose replicated form folds the arms' structural zeros away)
+    constexpr bool LNE = S > 1 && MAXV <= 12 && !(KINHIP_IKT_OWN) && KINHIP_IKT_LDSNE;
+    using NL = IktNe<MAXV, ROWS, (NR > 0 ? NR : 1) * S>;
+    constexpr int NJ = LNE ? (NL::NE + S - 1) / S : 1;
+    T* ne_reg = nullptr;
+    int eR[NJ], eC[NJ];
+    if constexpr (LNE) {
+        ne_reg = ikt_ne_lds<T, (64 / S) * NL::SIZE>() + (lane / S) * NL::SIZE;  // one region per S-lane group of the wave
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int e = sl + S * j;
+            int R = 0, C = 0;
+#pragma unroll
+            for (int r = 0; r < MAXV; ++r)
+                if (e >= NL::st(r)) {
+                    R = r;
+                    C = e - NL::st(r);
+                }
+            C = C == R + 1 ? MAXV : C;
+            eR[j] = e < NL::NE ? R : 0;
+            eC[j] = e < NL::NE ? C : 0;
+        }
+    }
     auto sdf_at = [&](T px, T py, T pz, T& d, T (&g)[3]) {  // the union (static or attached) at one point
         T xs[1] = {px}, ys[1] = {py}, zs[1] = {pz}, ds[1], gs[1][3];
         if constexpr (MAXG > 0) scene_union<T, true, 1, MG>(sc, boxes, aabb, xs, ys, zs, ds, gs, smem, use_lds);
@@ -533,11 +590,11 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
         }
         link_frame(Lf, Lf, P.has_xt != 0, P.Xt);
         KIN_IKT_STAMP(1);
+        uint64_t inband[NR > 0 ? NR : 1];  // S > 1: the lanes whose sphere of round r is inside the band
         if constexpr (S > 1) {
             // this lane's spheres: distance, gradient, row; then every in-band row into the system in
-            // sphere order, broadcast from its lane
+            // sphere order, broadcast from its lane (LNE: the rows to LDS, the system after the pose rows)
             T av[NR][MAXV], viol[NR];
-            uint64_t inband[NR];
             T dl = T(INFINITY);
             // every round's sphere of this lane in one pass over the union (its boxes loaded once; each
             // point's arithmetic is the one-point pass's)
@@ -564,8 +621,21 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
             }
             dmin = row_group_min<S>(dl);
             KIN_IKT_STAMP(2);
+            if constexpr (LNE) {  // this lane's sphere rows, zero outside the band (they then add exact zeros)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    T* row = ne_reg + (r * S + sl) * NL::RW;
+                    const bool inb = (inband[r] >> lane) & 1ull;
+#pragma unroll
+                    for (int v = 0; v < MAXV; ++v) {
+                        row[v] = inb ? w2 * av[r][v] : T(0);
+                        row[MAXV + v] = inb ? av[r][v] : T(0);
+                    }
+                    row[2 * MAXV] = inb ? viol[r] : T(0);
+                }
+            }
             KIN_IKT_UNROLL
-            for (int k = 0; k < P.n_sph; ++k) {
+            for (int k = 0; k < (LNE ? 0 : P.n_sph); ++k) {
                 const int r = k / S, src = gbase + k % S;
                 const uint32_t anc = sph[k].anc;  // (constant in the specialised kernel)
                 uint64_t bal = 0;
@@ -705,11 +775,52 @@ __device__ __forceinline__ void ikt_body(const KIkcProg<T>& P, const KIkcStep<T>
                 };
                 own(IntC<0>());
                 if constexpr (NRO > 1) own(IntC<1>());
+            } else if constexpr (LNE) {  // row r of J and e_r (every lane of the group the same values)
+                T* jr = ne_reg + NL::JB + r * NL::JW;
+#pragma unroll
+                for (int v = 0; v < MAXV; ++v) jr[v] = Jr[v];
+                jr[MAXV] = e[r];
             } else {
 #pragma unroll
                 for (int v = 0; v < MAXV; ++v)
                     if ((P.tgt_mask >> v) & 1u) bv[v] = fma(Jr[v], e[r], bv[v]);
                 lower_rank1<T, MAXV>(A, Jr, Jr, P.tgt_mask);
+            }
+        }
+        if constexpr (LNE) {
+            // this lane's entries: the in-band sphere rows in sphere order, then the pose rows; then the system
+            // back from every lane's entries (the group's lanes run in step: LDS accesses of a wave are in order)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            T acc[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[j] = T(0);
+            // (no branch per sphere: its reads then pipeline instead of one LDS round trip per in-band sphere)
+            KIN_IKT_UNROLL
+            for (int k = 0; k < P.n_sph; ++k) {
+                const T* row = ne_reg + k * NL::RW;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[j] = fma(row[eR[j]], row[MAXV + eC[j]], acc[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < ROWS; ++i) {
+                const T* jr = ne_reg + NL::JB + i * NL::JW;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) acc[j] = fma(jr[eR[j]], jr[eC[j]], acc[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (sl + S * j < NL::NE) ne_reg[NL::NB + sl + S * j] = acc[j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int v = 0; v < MAXV; ++v) {
+                const T* ar = ne_reg + NL::NB + NL::st(v);
+#pragma unroll
+                for (int c = 0; c <= v; ++c) A[v][c] = ar[c];
+                bv[v] = ar[v + 1];
             }
         }
         if constexpr (OWN) {  // gather the owned rows into every lane of the group (structural zeros stay 0)

@@ -25,6 +25,7 @@ from kinhip import _lib as K
 pytestmark = pytest.mark.gpu
 
 HIP_STREAM_PER_THREAD = 2
+HIP_ERROR_CAPTURED_EVENT = 907
 
 
 @pytest.fixture(scope="module")
@@ -100,8 +101,15 @@ def _run(config4, n_threads, streams, reps=6, sync="stream", concurrent=True):
             x.start()
             x.join(timeout=120)
     if sync == "event":
-        for ev in events:
-            assert hip.hipEventSynchronize(ev) == 0
+        for t, ev in enumerate(events):
+            rc = hip.hipEventSynchronize(ev)
+            if rc == HIP_ERROR_CAPTURED_EVENT and streams[t] == HIP_STREAM_PER_THREAD and not th[t].is_alive():
+                # the runtime defect the library guards against (kinhip_host.cpp ik_set_state): an event recorded
+                # on the per-thread stream of a thread that has exited may report hipErrorCapturedEvent
+                # (profiles/r06_gpu_tests_capturedevent.log); that exit drained the stream, so the read is complete
+                hip.hipGetLastError()
+                rc = 0
+            assert rc == 0, rc
     torch.cuda.synchronize()
     for ev in events:
         hip.hipEventDestroy(ev)

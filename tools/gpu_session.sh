@@ -162,6 +162,14 @@ for step in "$@"; do
       mkdir -p gpurun_out/jit
       timeout -k 10 200 env KINHIP_LIB=$AB KINHIP_JIT_DUMP=$PWD/gpurun_out/jit/coll AB_SPEC=1 \
         python -u tools/coll_spec_ab.py 2>&1 | quiet || exit 8 ;;
+    srcab=*)  # srcab=<tool.py>:<reps>: the A/B build with the JIT device headers of gpurun_ab/old vs csrc/, alternated
+      spec=${step#srcab=}; tool=${spec%%:*}; reps=${spec#*:}
+      for r in $(seq 1 $reps); do
+        for d in gpurun_ab/old kinematics.jl_amd/csrc; do
+          echo "[$d]"
+          timeout -k 10 300 env KINHIP_LIB=$AB KINHIP_JIT_SRC_DIR=$PWD/$d python -u tools/$tool 2>&1 | quiet || exit 8
+        done
+      done ;;
     ab=*)
       spec=${step#ab=}; w=${spec%%:*}; IFS=';' read -ra sets <<< "${spec#*:}"
       timeout -k 10 900 python -u tools/ab.py $w "${sets[@]}" 2>&1 | quiet || exit 8 ;;
