@@ -745,6 +745,12 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="batch-size sweep, unpadded rows, strong scaling")
     args = ap.parse_args()
 
+    # stdout carries the one JSON line only: RCCL prints its version banner to the process's stdout when the
+    # group initialises (a round-6 one-rank RCCL run had four such lines before the JSON), so until the line is
+    # printed file descriptor 1 points at stderr
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     # KINHIP_DIST_ALWAYS_GROUP=1 (torchrun --nproc-per-node 1): a one-rank RCCL group runs every
     # collective of the sharded path -- barriers, max over ranks, the result gathers, the strong-scaling
     # leg -- on the single-GPU box, exactly as each rank of an N-GPU run does
@@ -968,8 +974,12 @@ def main():
         out["specialization_errors"] = SPEC_ERRORS
     if rank == 0 and ws == 1 and not args.no_cpu:  # the CPU baseline is a single-GPU-run figure
         out["cpu_baseline"] = _cpu_baseline(m)
+    sys.stdout.flush()
+    os.dup2(json_fd, 1)
+    os.close(json_fd)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    os.dup2(2, 1)  # (nothing after the line: the group's teardown may print too)
     if ctx.dist:
         ctx.dist.destroy_process_group()
 
