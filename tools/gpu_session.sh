@@ -32,6 +32,11 @@
 #   scene-const                 door sweep A/B: scene tables as data vs compiled in (tools/scene_ab.py), x3 each,
 #                               plus a rocprofv3 kernel trace of both (VGPR counts)
 #   pts-probe                   tools/pts_probe (hipStreamPerThread after thread exit vs hipDeviceSynchronize)
+#   srcab=<tool.py>:<reps>      the A/B build's specialised kernels from the device headers of gpurun_ab/old (fill it
+#                               first: git show <rev>:kinematics.jl_amd/csrc/<h> > gpurun_ab/old/<h> for the six
+#                               kinhip_{prog,device,fk_dev,ik_dev,coll_dev,ikt_dev}.h) vs csrc/ (KINHIP_JIT_SRC_DIR),
+#                               alternated <reps> times; any KINHIP_JIT_SRC_DIR in the caller's environment also
+#                               applies to the other steps (e.g. ikt-sections)
 set -u -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
