@@ -864,14 +864,12 @@ def main():
             for lg, k_s in ((22, 10), (24, 5)):
                 w_b, d_b = timed_leg(torch.float32, True, [gl], args.layout, n=1 << lg, steps=k_s, warmup=2)
                 ach = bytes_per_eval * (1 << lg) / (d_b / k_s) / 1e9
-                pat_b = _pattern_us(8, 60, 1 << lg, args.tile, stream, reps=k_s, warmup=1,
-                                    per_lane=2 if lg >= 23 and args.spec else 1)
+                pat_b = _pattern_us(8, 60, 1 << lg, args.tile, stream, reps=k_s, warmup=1, per_lane=1)
                 big[f"2^{lg}"] = {"evals_per_s": (1 << lg) * ws * k_s / w_b, "avg_launch_us": d_b / k_s * 1e6,
                                   "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
                                   "pattern_ceiling_us": pat_b, "frac_of_pattern": pat_b / (d_b / k_s * 1e6),
                                   "working_set_MB": bytes_per_eval * (1 << lg) / 1e6,
-                                  "kernel": ("kinhip_jit_fks (grid-strided, 2 configurations per lane)"
-                                             if lg >= 23 and args.spec else "as the headline")}
+                                  "kernel": "as the headline (fp32 runs the one-per-lane grid at every size)"}
             out["roofline"]["large_batches"] = big
             out["roofline"]["rocprof_note"] = ("the cold-cache and 2^22 legs launch the headline kernel too (same name); "
                                                "tools/trace_headline.py splits a rocprofv3 kernel trace of this bench "

@@ -17,7 +17,7 @@ plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=torch.float32).specialize(
 res = []
 scrub = torch.ones(1 << 28, dtype=torch.float32, device=dev)
 ref = None
-for lg in (20, 22, 24):
+for lg in (20, 22, 24, 26):
     n = 1 << lg
     Q = kinhip.uniform_configs([j.lower_limit for j in arm], [j.upper_limit for j in arm], n, dtype=torch.float32,
                                device=dev)
