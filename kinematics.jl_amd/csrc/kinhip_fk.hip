@@ -59,21 +59,18 @@ __global__ __launch_bounds__(256) void k_pose_residual(const T* __restrict__ pos
 
 }  // namespace
 
-// fp64 batches from this size on run the grid-strided specialised k_fk (launch_fk); fp32 never does
-constexpr int64_t kFkStrideMin = int64_t(1) << 23;
 
 template <typename T>
 hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom& g, const T* q, int64_t ldq,
                      int64_t n, T* poses, int64_t ldp, T* jac, int64_t ldj, const TileArgs& ta, const JitFns* jf,
                      hipStream_t st) {
-    // Batches whose arrays far exceed the 256 MiB Infinity Cache run the grid-strided specialised
-    // kernel with 2 configurations per lane: the next configuration's angles are in flight while
-    // this one is computed and stored (2^24 fp32 FK + J: 799 -> 733 us; at 2^22 the two are within
-    // 1% (160 / 162 us) and at 2^20 the one-per-lane grid is faster: 41 vs 46 us; tools/fk_stride_ab.py,
-    // profiles/r02_fk_stride_ab.txt).
-    // Since the occupancy cap below (round 4) the one-per-lane fp32 grid is the faster one at every size: 2^24
-    // 670 vs 735 us, 2^26 2677 vs 2851 us, 2^20 / 2^22 equal (profiles/r06_fk_stride_ab.txt); fp32 keeps it, fp64
-    // (not re-measured) keeps the strided kernel from 2^23.
+    // Rounds 2-5 ran batches whose arrays far exceed the 256 MiB Infinity Cache (2^23 and up) on the
+    // grid-strided specialised kernel with 2 configurations per lane, the next configuration's angles in
+    // flight while this one is computed and stored (then 2^24 fp32 FK + J 799 -> 733 us; 2^20 41 vs 46 us for
+    // the one-per-lane grid; tools/fk_stride_ab.py, profiles/r02_fk_stride_ab.txt).
+    // Since the occupancy cap below (round 4) the one-per-lane grid is the faster one at every size, and only it
+    // runs: fp32 2^24 670 vs 735 us, 2^26 2677 vs 2851 us; fp64 2^24 1321 vs 1763 us, 2^26 5270 vs 6817 us; 2^20 /
+    // 2^22 equal (profiles/r06_fk_stride_ab.txt).  The grid-strided kernel stays for A/B runs:
     // KINHIP_FK_PER_LANE=<k> forces k configurations per lane (1: the plain kernel).
     static const int per_lane_env = [] {
         const int v = ab_env_int("KINHIP_FK_PER_LANE", 0);
@@ -98,8 +95,7 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         const int v = ab_env_int("KINHIP_FK_BLOCK", 0);
         return v == 64 || v == 128 || v == 256 ? v : 0;
     }();
-    const bool strided_auto = sizeof(T) == 8 && n >= kFkStrideMin;
-    const bool one_per_lane = !(per_lane_env > 1 || (strided_auto && jf && jf->fk_stride && !per_lane_env));
+    const bool one_per_lane = !(per_lane_env > 1);
     const int want = fk_block_env ? fk_block_env : (sizeof(T) == 8 && one_per_lane ? 128 : g.block);
     const int blk = jf && jf->fk && (ta.tile >= n || ta.tile % want == 0) ? want : g.block;  // (tiles: whole blocks)
     // plain SoA (tile >= n): chunks are element offsets along the rows; tiled: whole tiles per chunk
@@ -115,7 +111,7 @@ hipError_t launch_fk(const KProg<T>& P, const KStep<T>* steps, const LaunchGeom&
         T* pc = poses ? poses + tp : poses;
         T* jc = jac ? jac + tj : jac;
         if (jf && jf->fk) {
-            const int per_lane = per_lane_env ? per_lane_env : (strided_auto && jf->fk_stride ? 2 : 1);
+            const int per_lane = per_lane_env ? per_lane_env : 1;
             const hipFunction_t jit = per_lane > 1 && jf->fk_stride ? jf->fk_stride : jf->fk;
             const unsigned gx = jit == jf->fk ? grid.x : (grid.x + per_lane - 1) / per_lane;
             int64_t cc = c;

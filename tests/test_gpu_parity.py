@@ -290,10 +290,10 @@ def test_specialized_fk_equals_generic(dev, fetch_tree, dtype, with_base, rpy_ja
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("with_base", [False, True])
 def test_specialized_strided_large_batch(dev, with_base, dt):
-    """Batches of >= 2^23 configurations: fp64 runs the grid-strided specialised k_fk (two configurations
-    per lane, the next one's angles prefetched; launch_fk), fp32 the one-per-lane grid (the faster one at every
-    size since round 4's occupancy cap, profiles/r06_fk_stride_ab.txt) -- both equal to the generic kernel on
-    plain and tiled layouts, with a partial last unit and a partial last tile, and phase-B links in the plan."""
+    """Batches of >= 2^23 configurations (which rounds 2-5 ran on a grid-strided specialised k_fk; since round 6
+    the one-per-lane grid at every size, the faster one in both precisions, profiles/r06_fk_stride_ab.txt; a
+    launch chunk is 2^27): equal to the generic kernel on plain and tiled layouts, with a partial last unit and
+    a partial last tile, and phase-B links in the plan."""
     m, arm = _fetch(with_base)
     gl = m.find_link("gripper_link")
     links = [gl, m.find_link("wrist_flex_link"), m.find_link("head_camera_rgb_optical_frame")]
