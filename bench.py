@@ -131,11 +131,13 @@ def fridge_scene():
     return m, [m.find_joint(n_) for n_ in ARM], sscc, sdf
 
 
-def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=20, spec=1, dt=torch.float32, over=None):
+def _ik_leg(m, arm, gl, ctx, stream, n=65536, reps=100, spec=1, dt=torch.float32, over=None):
     """Config 4: batched DLS IK, `n` reachable targets per GPU (FK of seeded random q), q0 = 0,
     <= 64 iterations with 3 seeded restarts; success = converged to |dp| < 1e-3 and |rot| < 1e-3.
     Multi-GPU: the solutions (8 angles) and iteration counts are all-gathered to every rank over
-    RCCL afterwards -- timed separately, not part of the solve rate."""
+    RCCL afterwards -- timed separately, not part of the solve rate.  `reps` back-to-back batches in the timed
+    region (100: its fixed start and stop, ~70 us, were 5% of the 20 batches timed before round 6's last bench;
+    tools/ik_host_probe.py: 66.3-67.4 us per batch over 200, host submission 10-15 us per call)."""
     plan = m.plan(arm, out_links=[gl], jac_link=gl, dtype=dt)
     if spec:
         _specialize(plan, kinhip.KIN_SPEC_FK | kinhip.KIN_SPEC_IK)
@@ -953,7 +955,7 @@ def main():
         # the error-scaled damping (kin_ik_params.damp_err) for comparison
         out["config4_ik_dls_damped"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec,
                                                over=dict(max_step=1.0, damp_err=0.01))
-        out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=3, spec=args.spec)
+        out["ik_dls_1M_targets"] = _ik_leg(m, arm, gl, ctx, stream, n=1 << 20, reps=10, spec=args.spec)
         out["config4_ik_dls_f64"] = _ik_leg(m, arm, gl, ctx, stream, spec=args.spec, dt=torch.float64)
         out["config5_fk_sdf"] = _coll_leg(ctx, stream, N, max(5, args.steps // 2), spec=args.spec, pad=args.row_pad)
         out["config5_fk_sdf"]["min_dist"]["pmc"] = _pmc_valu("pmc_coll32s.json")

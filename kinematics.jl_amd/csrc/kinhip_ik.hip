@@ -143,7 +143,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
         T* ec = err ? err + s0 : err;
         if (at.trace) ar.trace = at.trace + s0;
         const hipFunction_t jk =
-            jf ? jf->ik[a.with_rot ? 1 : 0][GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3] : nullptr;
+            jf ? jf->ik[a.with_rot == 2 ? 2 : a.with_rot ? 1 : 0][GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3] : nullptr;
         if (jk) {
             int64_t cc = c, pw = per_wave;
             void* args[] = {(void*)&ar, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
@@ -214,7 +214,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             if (sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3 && KINHIP_IK_F64_ITERS > 0 && tpq_env < 0 && qmode < 0)
                 q1 = false;
             if (q1 && tpq_env < 0 && qmode < 0 && jf) {
-                const hipFunction_t f1 = jf->ik[a.with_rot ? 1 : 0][0];
+                const hipFunction_t f1 = jf->ik[a.with_rot == 2 ? 2 : a.with_rot ? 1 : 0][0];
                 int nb = 0;
                 if (f1 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f1, 256, 0) == hipSuccess &&
                     (int64_t)nb * 4 * cus > resident_waves)
@@ -250,7 +250,7 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             const int bs2 = p2_block_env == 64 ? 64 : 256;
             a2.p2_spread = 0;
             if (spread_env != 0 && bs2 == 256 && jf) {  // (the resident workgroups of the phase-2 kernel)
-                const hipFunction_t f2 = jf->ik[a.with_rot ? 1 : 0][G2 == 1 ? 0 : G2 == 2 ? 1 : G2 == 4 ? 2 : 3];
+                const hipFunction_t f2 = jf->ik[a.with_rot == 2 ? 2 : a.with_rot ? 1 : 0][G2 == 1 ? 0 : G2 == 2 ? 1 : G2 == 4 ? 2 : 3];
                 int nb = 0;
                 if (f2 && hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f2, 256, 0) == hipSuccess && nb > 0 &&
                     (nb <= 2 || spread_env > 1))

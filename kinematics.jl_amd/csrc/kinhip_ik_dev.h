@@ -241,6 +241,11 @@ struct IkArgsT {
     const T* q_alt;
 };
 
+// the objective inside ik_body: RPY < 0 reads it from the launch (IkArgsT::rpy_obj, the generic kernels); the
+// specialised kernels compile it in (RPY = 0 axis-angle or position, 1 the reference's rpy objective): the
+// iteration then carries neither the other objective's code nor the register copies that join the two paths
+// (config 4: 0.072-0.075 -> 0.068-0.070 ms, identical results; profiles/r06_ik_rpy_const_ab.txt)
+#define KIN_RPY(a) (RPY < 0 ? (a).rpy_obj != 0 : RPY != 0)
 // lambda^2 + mu (ep^2 + er^2) rounded operation by operation, as the oracle forms it (no contraction)
 template <typename S>
 __device__ __forceinline__ S ik_damping(S lam2, S mu, S ep, S er) {
@@ -328,7 +333,7 @@ __device__ __forceinline__ int group_min(int v) {
 // writes the result and takes the wave's next target at once, so a wave no
 // longer waits for its slowest target before the others move on.  The queue is
 // wave-local (ballot + popcount, no atomics, nothing in memory between launches).
-template <typename T, int MAXA, int ROWS, int G>
+template <typename T, int MAXA, int ROWS, int G, int RPY = -1>
 __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __restrict__ S, const IkArgsT<T>& a,
                                         const T* __restrict__ tgt, int64_t ldt, T* __restrict__ q, int64_t ldq,
                                         int64_t n, int32_t* __restrict__ iters, T* __restrict__ err, int64_t lde,
@@ -392,7 +397,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             for (int c = 0; c < 3; ++c) Rt[3 * r + c] = KIN_IK_LD(tgt, r + 3 * c, ldt, off);
             pt[r] = KIN_IK_LD(tgt, 9 + r, ldt, off);
         }
-        if (ROWS == 6 && a.rpy_obj) {
+        if (ROWS == 6 && KIN_RPY(a)) {
             T kk[6];
             rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Rt, trpy, kk);
         }
@@ -548,7 +553,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
         T kr[6];  // rpy_derivative! coefficients (reference objective)
         if constexpr (ROWS == 6) {
             T w[3];
-            if (a.rpy_obj) {  // wave-uniform
+            if (KIN_RPY(a)) {  // wave-uniform
                 T r[3];
                 rpy_and_rate<KINHIP_IK_FAST_ATAN != 0>(Lf.r, r, kr);
 #pragma unroll
@@ -601,7 +606,7 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             ro[s][2] = fma(rz[s][0], dy, -(rz[s][1] * dx));
         }
         if constexpr (ROWS == 6) {
-            if (a.rpy_obj) {  // angular rows -> d(rpy)/dq (get_jacobian!(...; rpy_jac=true))
+            if (KIN_RPY(a)) {  // angular rows -> d(rpy)/dq (get_jacobian!(...; rpy_jac=true))
 #pragma unroll
                 for (int s = 0; s < MAXA; ++s) {
                     if (S[s].jkind == MOT_PRISM) continue;  // [z; 0]: its linear part is z itself

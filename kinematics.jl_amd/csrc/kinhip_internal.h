@@ -51,7 +51,7 @@ inline TileArgs plain_soa(int64_t n) { return TileArgs{n, 0, 0, 0, 0}; }
 struct JitFns {
     hipFunction_t fk = nullptr;
     hipFunction_t fk_stride = nullptr;  // the same, grid-strided with prefetched angles (launch_fk)
-    hipFunction_t ik[2][4] = {};  // [rows == 6][log2 of lanes per target]
+    hipFunction_t ik[3][4] = {};  // [0: rows 3, 1: rows 6 axis-angle, 2: rows 6 rpy objective][log2 of lanes per target]
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
     hipFunction_t coll_scene[2][2] = {};  // the same over an attached union [with gradients][up to 2 | 4 groups]
