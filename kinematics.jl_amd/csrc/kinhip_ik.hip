@@ -135,15 +135,16 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
     // automatic (only where the queue's resident waves do not lower the kernel's occupancy)
     static const int tpq_env = ab_env_int("KINHIP_IK_TP_QUEUE", -1);
     auto one = [&](IkArgsT<T>& ar, int GG, int64_t s0, int64_t c, int64_t per_wave, int64_t nw,
-                   int bs = 256) -> hipError_t {
+                   int bs = 256, bool no_f64 = false) -> hipError_t {
         const dim3 grid((unsigned)((nw * 64 + bs - 1) / bs)), block(bs);
         const T* tc = target + s0;
         T* qc = q + s0;
         int32_t* ic = iters ? iters + s0 : iters;
         T* ec = err ? err + s0 : err;
         if (at.trace) ar.trace = at.trace + s0;
-        const hipFunction_t jk =
-            jf ? jf->ik[a.with_rot == 2 ? 2 : a.with_rot ? 1 : 0][GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3] : nullptr;
+        const int vr = a.with_rot == 2 ? 2 : a.with_rot ? 1 : 0, vg = GG == 1 ? 0 : GG == 2 ? 1 : GG == 4 ? 2 : 3;
+        // (no_f64: the phase-2 kernel without the fp64 solve, where the launch never takes it -- see below)
+        const hipFunction_t jk = !jf ? nullptr : no_f64 && jf->ik2[vr][vg] ? jf->ik2[vr][vg] : jf->ik[vr][vg];
         if (jk) {
             int64_t cc = c, pw = per_wave;
             void* args[] = {(void*)&ar, (void*)&tc, (void*)&ldt, (void*)&qc, (void*)&ldq, (void*)&cc,
@@ -259,7 +260,14 @@ hipError_t launch_ik_dls(const KProg<T>& P, const KStep<T>* steps, const LaunchG
             }
             a2.fail_ctl = scr.fail_ctl;
             a2.fail_mask = (uint32_t)(scr.ring_cap - 1);
-            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2, bs2)) != hipSuccess) {
+            // Phase 2 never takes the fp32 kernels' fp64 solve (ik_body: attempt 0 before iteration
+            // KINHIP_IK_F64_ITERS, or lambda^2 below KINHIP_IK_F32SOLVE_MIN_LAM2) when attempt 0 resumes at or past
+            // that iteration and lambda is not below the threshold: its specialised form without that code
+            // (F64S = false; the same arithmetic) then runs -- config 4 0.072-0.074 -> 0.070 ms on one box,
+            // identical results (profiles/r06_ik_p2_nof64_ab.txt)
+            const bool no_f64 = sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3 &&
+                                !(at.lam2 < T(KINHIP_IK_F32SOLVE_MIN_LAM2)) && (cut == 0 || cut >= KINHIP_IK_F64_ITERS);
+            if ((e = one(a2, G2, s0, c, ng2, (c + ng2 - 1) / ng2, bs2, no_f64)) != hipSuccess) {
                 // phase 1 ran but phase 2 did not move the next call's start mark: restart the ring;
                 // the targets phase 1 did not solve keep undefined outputs (kin_ik_dls_batch says so)
                 (void)hipMemsetAsync(scr.fail_ctl, 0, sizeof(uint32_t) * kIkCtlStride * kIkSubRings, st);

@@ -333,7 +333,7 @@ __device__ __forceinline__ int group_min(int v) {
 // writes the result and takes the wave's next target at once, so a wave no
 // longer waits for its slowest target before the others move on.  The queue is
 // wave-local (ballot + popcount, no atomics, nothing in memory between launches).
-template <typename T, int MAXA, int ROWS, int G, int RPY = -1>
+template <typename T, int MAXA, int ROWS, int G, int RPY = -1, bool F64S = true>
 __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __restrict__ S, const IkArgsT<T>& a,
                                         const T* __restrict__ tgt, int64_t ldt, T* __restrict__ q, int64_t ldq,
                                         int64_t n, int32_t* __restrict__ iters, T* __restrict__ err, int64_t lde,
@@ -839,9 +839,14 @@ __device__ __forceinline__ void ik_body(const KProg<T>& P, const KStep<T>* __res
             }
         };
         if constexpr (sizeof(T) == 4 && KINHIP_IK_F64SOLVE == 3) {
-            // fp64 for the first iterations of attempt 0 (the caller's q0), fp32 elsewhere (see the macro)
-            if ((att == 0 && it < KINHIP_IK_F64_ITERS) || a.lam2 < T(KINHIP_IK_F32SOLVE_MIN_LAM2)) damped_solve(double());
-            else damped_solve(float());
+            // fp64 for the first iterations of attempt 0 (the caller's q0), fp32 elsewhere (see the macro).  F64S =
+            // false: a launch where that never holds (phase 2 of the two-phase schedule with a hand-over point of at
+            // least KINHIP_IK_F64_ITERS and lambda^2 >= KINHIP_IK_F32SOLVE_MIN_LAM2; launch_ik_dls) compiles the fp64
+            // solve out -- the same arithmetic, without its code and registers in the loop
+            if (F64S && ((att == 0 && it < KINHIP_IK_F64_ITERS) || a.lam2 < T(KINHIP_IK_F32SOLVE_MIN_LAM2)))
+                damped_solve(double());
+            else
+                damped_solve(float());
         } else {
             damped_solve(typename ik_solve_type<sizeof(T) == 4 && KINHIP_IK_F64SOLVE != 1>::type());
         }

@@ -52,6 +52,7 @@ struct JitFns {
     hipFunction_t fk = nullptr;
     hipFunction_t fk_stride = nullptr;  // the same, grid-strided with prefetched angles (launch_fk)
     hipFunction_t ik[3][4] = {};  // [0: rows 3, 1: rows 6 axis-angle, 2: rows 6 rpy objective][log2 of lanes per target]
+    hipFunction_t ik2[3][4] = {};  // the same without the fp64 solve (phase 2 of launch_ik_dls; G >= 2 only)
     hipFunction_t nakamura = nullptr;
     hipFunction_t coll[2] = {};   // [with gradients]
     hipFunction_t coll_scene[2][2] = {};  // the same over an attached union [with gradients][up to 2 | 4 groups]
